@@ -1,0 +1,116 @@
+/* whisper_mi355.h — C-ABI of the MI355X (gfx950) Whisper engine, libwhisper_mi355.so.
+ *
+ * The drop-in boundary is faster-whisper's `WhisperModel(...).transcribe(...)` as the vlog transcription
+ * worker calls it (reference `worker/transcription.py:78-111`).  Below that call, faster-whisper drives
+ * CTranslate2's C++ `models.Whisper` (encode / generate / detect_language / align) [FW↑]; this library
+ * replaces that C++ seam, plus faster-whisper's numpy log-mel.  The Python host (vlog_amd/) mirrors the
+ * faster-whisper surface on top of these entry points and owns all input/output device buffers
+ * (PyTorch-ROCm tensors); the engine owns the weights, the KV caches and its scratch.
+ *
+ * Conventions: every function returns 0 on success and -1 on failure (never aborts); the message is
+ * available from wm_last_error() (thread-local).  Every call sets the engine's device itself, so calls may
+ * come from any thread (the worker runs `transcribe` on a ThreadPoolExecutor thread,
+ * worker/transcription.py:361-369); calls on one engine are serialised by an internal lock.  Pointers
+ * named d_* are device pointers; h_* are host pointers.  `stream` is a hipStream_t (NULL = null stream).
+ */
+#ifndef WHISPER_MI355_H
+#define WHISPER_MI355_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct wm_engine wm_engine;
+
+typedef struct wm_model_dims {
+  int32_t n_mels, n_state, n_head, n_enc_layer, n_dec_layer, n_vocab, n_audio_ctx, n_text_ctx;
+  int32_t eot, sot, no_speech, no_timestamps, timestamp_begin, blank;
+} wm_model_dims;
+
+/* Replaces ctranslate2.models.Whisper(model_path, device, compute_type) as constructed by
+ * faster_whisper.WhisperModel.__init__ [FW↑] (called at worker/transcription.py:81-85). */
+int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out);
+void wm_destroy(wm_engine* e);
+const char* wm_last_error(void);
+int32_t wm_abi_version(void);
+
+/* Weight upload into the engine's packed layout (names and layouts: see INTEGRATION.md §Weights).
+ * d_src must hold exactly nbytes (bf16 matrices, f32 vectors). */
+int wm_set_weight(wm_engine* e, const char* name, const void* d_src, int64_t nbytes, void* stream);
+/* 1 when every weight has been set. */
+int32_t wm_weights_complete(wm_engine* e);
+
+/* Log-mel, replacing faster-whisper FeatureExtractor.__call__ [FW↑] (reached from
+ * worker/transcription.py:105).  Computes frames [frame0, frame0+n_frames) of the WHOLE-FILE spectrogram
+ * (file of n_samples samples; d_pcm[i] is file sample pcm_offset+i) as log10(max(mel, 1e-10)) into
+ * d_mel[m*ld + f], and folds their maximum into *d_gmax (order-preserving uint32, zero-initialised by the
+ * caller).  wm_logmel_finalize applies max(x, gmax-8), (x+4)/4 in place; gmax is taken from h_gmax when
+ * non-NULL (cross-shard max), else from d_gmax. */
+int wm_logmel(wm_engine* e, const float* d_pcm, int64_t pcm_offset, int64_t n_samples, int64_t frame0,
+              int32_t n_frames, float* d_mel, int64_t ld, uint32_t* d_gmax, void* stream);
+int wm_logmel_finalize(wm_engine* e, float* d_mel, int64_t n_frames, int64_t ld, const uint32_t* d_gmax,
+                       const float* h_gmax, float* h_gmax_out, void* stream);
+
+/* Encoder, replacing ctranslate2 Whisper.encode(features) [FW↑] (faster-whisper generate_segments).
+ * Window b reads mel frames [h_seek[b], h_seek[b]+h_nframes[b]) of d_mel (ld = frames per mel row) and
+ * zero-pads to 3000 frames (faster-whisper pad_or_trim).  Output bf16 [B][1500][n_state]. */
+int wm_encode(wm_engine* e, const float* d_mel, int64_t ld, const int32_t* h_seek, const int32_t* h_nframes,
+              int32_t B, void* d_enc_out, void* stream);
+
+/* Capacity of the decoder state: n_slots windows of cross-KV, n_hyp hypotheses of self-KV. */
+int wm_reserve(wm_engine* e, int32_t n_slots, int32_t n_hyp, void* stream);
+
+/* Cross-attention K/V projection of B encoder outputs into slots [slot0, slot0+B) (all decoder layers;
+ * CTranslate2 computes these inside generate [FW↑]). */
+int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void* stream);
+
+/* ctranslate2 Whisper.generate(encoder_output, prompts, ...) [FW↑] as faster-whisper
+ * generate_with_fallback calls it: all windows share one prompt length; greedy (beam_size 1,
+ * temperature 0), beam search (beam_size > 1, patience, length_penalty) or sampling (temperature > 0,
+ * num_hypotheses = best_of).  Logit rules, log-softmax and selection run on the device. */
+typedef struct wm_generate_args {
+  int32_t n_windows;
+  const int32_t* h_slots;        /* [n_windows] cross-KV slot of each window */
+  int32_t prompt_len;
+  const int32_t* h_prompts;      /* [n_windows][prompt_len] */
+  int32_t sot_index;             /* position of <|startoftranscript|> in the prompt; -1: no no_speech_prob */
+  int32_t beam_size;
+  float patience;
+  float length_penalty;
+  int32_t max_length;            /* total decoder length including the prompt (<= n_text_ctx) */
+  float temperature;             /* > 0: sampling */
+  int32_t num_hypotheses;        /* sampling: best_of */
+  uint64_t seed;
+  const int32_t* h_suppress;     /* suppressed token ids */
+  int32_t n_suppress;
+  int32_t suppress_blank;
+  int32_t max_initial_timestamp_index;   /* < 0: none */
+  int32_t with_timestamps;
+  int32_t check_every;           /* steps between host checks for completion (>= 1) */
+  /* outputs (host) */
+  int32_t* h_tokens;             /* [n_windows][max_length] generated tokens (no prompt, no <|endoftext|>) */
+  int32_t* h_lengths;            /* [n_windows] */
+  float* h_scores;               /* [n_windows] cum_logprob / len^length_penalty (CTranslate2 score) */
+  float* h_cum_logprob;          /* [n_windows] */
+  float* h_no_speech;            /* [n_windows] */
+  int32_t* h_steps;              /* [1] decoder steps run (incl. prefill) */
+} wm_generate_args;
+int wm_generate(wm_engine* e, const wm_generate_args* a, void* stream);
+
+/* Teacher-forced decoder forward over n_seq sequences of seq_len tokens (one window slot each): logits for
+ * every position (d_logits f32 [n_seq*seq_len][n_vocab]) or only the last (last_only: [n_seq][n_vocab]).
+ * Optional cross-attention capture for word alignment (ctranslate2 Whisper.align [FW↑]): for each of
+ * n_align (layer, head) pairs in h_align_heads, softmax weights are written to
+ * d_attn[((s*seq_len + p)*n_align + a)*1500 + t].  Also serves detect_language ([sot], last_only). */
+int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_len, const int32_t* h_tokens,
+               float* d_logits, int32_t last_only, const int32_t* h_align_heads, int32_t n_align, float* d_attn,
+               void* stream);
+
+/* Bytes of device memory held by the engine (weights + caches + scratch). */
+int64_t wm_device_bytes(wm_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

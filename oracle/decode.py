@@ -1,0 +1,236 @@
+"""Logit rules, greedy / beam / sampling search, language detection (TEST INFRASTRUCTURE ONLY).
+
+Restates CTranslate2 `Whisper.generate` / `detect_language` as faster-whisper drives them from
+`generate_with_fallback` / `detect_language` [FW↑ 1.1.x] (reference call `worker/transcription.py:105-111`):
+
+  rules per step, in this order (openai `DecodingTask._get_logit_filters`, CT2 logits processors):
+    1. SuppressBlank  — at the first sampled step suppress " " (blank) and <|endoftext|>
+    2. SuppressTokens — the faster-whisper suppress list (config non-speech ids + special tokens)
+    3. ApplyTimestampRules — pinned against transformers `WhisperTimeStampLogitsProcessor`
+       ([TF] generation/logits_process.py:1909-2049): suppress <|notimestamps|>; pairs; monotonicity;
+       first token a timestamp <= max_initial_timestamp_index; timestamp logsumexp > max text logprob
+       forces a timestamp.
+  greedy   — argmax of the rule-masked log-softmax; score = cumulative logprob (incl. <|endoftext|>)
+             / len(tokens)**length_penalty (CT2 normalisation; faster-whisper recovers
+             avg_logprob = score * len**lp / (len + 1)).
+  beam     — openai `BeamSearchDecoder` semantics (each beam proposes its top beam+1 tokens; candidates are
+             ranked by cumulative logprob; finished ones are collected until round(beam * patience);
+             final choice by score / len**length_penalty).
+  no_speech_prob — softmax of the raw logits at the <|startoftranscript|> position, token <|nospeech|>.
+  max_length counts the prompt (faster-whisper passes max_length=448 and max_new_tokens + len(prompt)).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+NEG_INF = -np.inf
+
+
+def log_softmax(x: np.ndarray) -> np.ndarray:
+    x = np.asarray(x, dtype=np.float64)
+    m = np.max(x, axis=-1, keepdims=True)
+    m = np.where(np.isfinite(m), m, 0.0)
+    return x - m - np.log(np.sum(np.exp(x - m), axis=-1, keepdims=True))
+
+
+def apply_rules(logits: np.ndarray, sampled: Sequence[int], st, suppress_tokens: Sequence[int],
+                suppress_blank: bool, max_initial_timestamp_index: Optional[int],
+                with_timestamps: bool = True) -> np.ndarray:
+    """logits [V] for ONE hypothesis; `sampled` = tokens generated after the prompt."""
+    x = np.array(logits, dtype=np.float64, copy=True)
+    first = len(sampled) == 0
+    if suppress_blank and first:
+        x[st.blank] = NEG_INF
+        x[st.eot] = NEG_INF
+    if len(suppress_tokens):
+        x[np.asarray(suppress_tokens, dtype=np.int64)] = NEG_INF
+    if not with_timestamps:
+        return x
+    tb = st.timestamp_begin
+    x[st.no_timestamps] = NEG_INF
+    last_ts = len(sampled) >= 1 and sampled[-1] >= tb
+    pen_ts = len(sampled) < 2 or sampled[-2] >= tb
+    if last_ts:
+        if pen_ts:
+            x[tb:] = NEG_INF
+        else:
+            x[: st.eot] = NEG_INF
+    ts = [t for t in sampled if t >= tb]
+    if ts:
+        last = ts[-1] if (last_ts and not pen_ts) else ts[-1] + 1
+        x[tb:last] = NEG_INF
+    if first:
+        x[:tb] = NEG_INF
+        if max_initial_timestamp_index is not None:
+            x[tb + max_initial_timestamp_index + 1:] = NEG_INF
+    lp = log_softmax(x)
+    ts_lp = np.logaddexp.reduce(lp[tb:])
+    if ts_lp > np.max(lp[:tb]):
+        x[:tb] = NEG_INF
+    return x
+
+
+@dataclass
+class GenerateResult:
+    tokens: List[int]
+    score: float
+    no_speech_prob: float
+    cum_logprob: float = 0.0
+    all_hypotheses: List[List[int]] = field(default_factory=list)
+
+
+@dataclass
+class GenerateOptions:
+    beam_size: int = 1
+    patience: float = 1.0
+    length_penalty: float = 1.0
+    max_length: int = 448
+    suppress_tokens: Sequence[int] = ()
+    suppress_blank: bool = True
+    max_initial_timestamp_index: Optional[int] = 50
+    with_timestamps: bool = True
+    sampling_temperature: float = 0.0
+    num_hypotheses: int = 1
+    seed: int = 0
+
+
+def _norm(cum: float, n: int, lp: float) -> float:
+    return cum / (max(n, 1) ** lp)
+
+
+def _prefill(model, cross, prompt: Sequence[int], st):
+    toks = np.asarray([list(prompt)], dtype=np.int64)
+    logits, cache = model.decode(toks, cross)
+    no_speech = 0.0
+    if st.sot in prompt:
+        sot_idx = list(prompt).index(st.sot)
+        p = np.exp(log_softmax(logits[0, sot_idx]))
+        no_speech = float(p[st.no_speech])
+    return logits[0, -1], cache, no_speech
+
+
+def generate_one(model, cross, prompt: Sequence[int], st, opt: GenerateOptions) -> GenerateResult:
+    """One window.  `cross` = model.cross_kv(enc[None]) for that window."""
+    if opt.sampling_temperature > 0:
+        return _sample(model, cross, prompt, st, opt)
+    if opt.beam_size > 1:
+        return _beam(model, cross, prompt, st, opt)
+    last_logits, cache, no_speech = _prefill(model, cross, prompt, st)
+    sampled: List[int] = []
+    cum = 0.0
+    pos = len(prompt)
+    finished = False
+    while pos < opt.max_length:
+        x = apply_rules(last_logits, sampled, st, opt.suppress_tokens, opt.suppress_blank,
+                        opt.max_initial_timestamp_index, opt.with_timestamps)
+        lp = log_softmax(x)
+        tok = int(np.argmax(lp))
+        cum += float(lp[tok])
+        if tok == st.eot:
+            finished = True
+            break
+        sampled.append(tok)
+        if pos + 1 >= opt.max_length:
+            break
+        logits, cache = model.decode(np.asarray([[tok]]), cross, cache, offset=pos)
+        last_logits = logits[0, -1]
+        pos += 1
+    del finished
+    return GenerateResult(sampled, _norm(cum, len(sampled), opt.length_penalty), no_speech, cum)
+
+
+def _beam(model, cross, prompt, st, opt: GenerateOptions) -> GenerateResult:
+    K = opt.beam_size
+    max_cand = int(round(K * opt.patience))
+    last_logits, cache, no_speech = _prefill(model, cross, prompt, st)
+    # replicate the prefill state for K beams
+    cache = [(np.repeat(k, K, 0), np.repeat(v, K, 0)) for k, v in cache]
+    logits_rows = np.repeat(last_logits[None], K, 0)
+    seqs: List[List[int]] = [[] for _ in range(K)]
+    sums = np.array([0.0] + [NEG_INF] * (K - 1))      # only beam 0 is live at the first step
+    finished: dict = {}
+    pos = len(prompt)
+    while True:
+        cands = []
+        for j in range(K):
+            if not np.isfinite(sums[j]):
+                continue
+            x = apply_rules(logits_rows[j], seqs[j], st, opt.suppress_tokens, opt.suppress_blank,
+                            opt.max_initial_timestamp_index, opt.with_timestamps)
+            lp = log_softmax(x)
+            top = np.argsort(-lp, kind="stable")[: K + 1]
+            for t in top:
+                cands.append((sums[j] + lp[t], j, int(t)))
+        cands.sort(key=lambda c: -c[0])
+        new_seqs, new_src, new_sums, new_fin = [], [], [], []
+        for score, j, t in cands:
+            if t == st.eot:
+                new_fin.append((score, tuple(seqs[j])))
+            else:
+                new_seqs.append(seqs[j] + [t]); new_src.append(j); new_sums.append(score)
+                if len(new_seqs) == K:
+                    break
+        for score, s in new_fin:
+            if len(finished) >= max_cand:
+                break
+            finished.setdefault(s, score)
+        pos += 1
+        if len(finished) >= max_cand or pos >= opt.max_length or not new_seqs:
+            if len(finished) < K:
+                for score, s in sorted(zip(new_sums, new_seqs), key=lambda z: -z[0]):
+                    if len(finished) >= K:
+                        break
+                    finished.setdefault(tuple(s), score)
+            break
+        while len(new_seqs) < K:
+            new_seqs.append(list(new_seqs[0])); new_src.append(new_src[0]); new_sums.append(NEG_INF)
+        src = np.asarray(new_src)
+        cache = [(k[src], v[src]) for k, v in cache]
+        seqs = new_seqs
+        sums = np.asarray(new_sums)
+        toks = np.asarray([[s[-1]] for s in seqs])
+        logits, cache = model.decode(toks, cross, cache, offset=pos - 1)
+        logits_rows = logits[:, -1]
+    ranked = sorted(finished.items(), key=lambda kv: -_norm(kv[1], len(kv[0]), opt.length_penalty))
+    best, cum = ranked[0]
+    return GenerateResult(list(best), _norm(cum, len(best), opt.length_penalty), no_speech, cum,
+                          [list(s) for s, _ in ranked])
+
+
+def _sample(model, cross, prompt, st, opt: GenerateOptions) -> GenerateResult:
+    rng = np.random.default_rng(opt.seed)
+    results = []
+    for _ in range(max(1, opt.num_hypotheses)):
+        last_logits, cache, no_speech = _prefill(model, cross, prompt, st)
+        sampled, cum, pos = [], 0.0, len(prompt)
+        while pos < opt.max_length:
+            x = apply_rules(last_logits, sampled, st, opt.suppress_tokens, opt.suppress_blank,
+                            opt.max_initial_timestamp_index, opt.with_timestamps)
+            lp = log_softmax(x)
+            p = np.exp(log_softmax(x / opt.sampling_temperature))
+            tok = int(rng.choice(len(p), p=p / p.sum()))
+            cum += float(lp[tok])
+            if tok == st.eot:
+                break
+            sampled.append(tok)
+            if pos + 1 >= opt.max_length:
+                break
+            logits, cache = model.decode(np.asarray([[tok]]), cross, cache, offset=pos)
+            last_logits = logits[0, -1]
+            pos += 1
+        results.append(GenerateResult(sampled, _norm(cum, len(sampled), opt.length_penalty), no_speech, cum))
+    results.sort(key=lambda r: -r.score)
+    return results[0]
+
+
+def detect_language(model, cross, st) -> List[tuple]:
+    """CT2 `detect_language`: one step from [sot]; softmax restricted to the language tokens.
+    -> [(code, prob)] sorted by probability (descending)."""
+    logits, _ = model.decode(np.asarray([[st.sot]]), cross)
+    lang = logits[0, 0, st.lang_begin: st.lang_begin + st.n_langs].astype(np.float64)
+    p = np.exp(log_softmax(lang))
+    order = np.argsort(-p, kind="stable")
+    return [(st.lang_codes[i], float(p[i])) for i in order]

@@ -1,0 +1,159 @@
+"""Whisper encoder/decoder forward in numpy (TEST INFRASTRUCTURE ONLY — see oracle/__init__.py).
+
+Restates what CTranslate2's `models.Whisper.encode` / `generate` compute [FW↑] (the reference reaches them
+through `worker/transcription.py:105-111`).  The architecture is pinned against transformers 5.15.0
+`WhisperForConditionalGeneration` ([TF] `models/whisper/modeling_whisper.py:241-798`) on identical seeded
+weights (tests/test_oracle_model.py):
+
+  encoder: conv1(k3,p1)+GELU(erf), conv2(k3,s2,p1)+GELU, + sinusoidal positions, L x pre-LN block
+           (MHA non-causal, k_proj without bias; MLP d->4d->d GELU), final LN (eps 1e-5)
+  decoder: token embedding + learned positions, L x pre-LN block (causal self-attn with KV cache,
+           cross-attn over the 1500 encoder positions, MLP), final LN, logits = h @ E^T (tied)
+
+Weights are a dict in HF naming (vlog_amd/weights.py produces it); the computation runs in float32 (or
+float64) on whatever values are given — the GPU engine stores the same values in bf16, so tests feed the
+oracle the bf16-rounded weights.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+from scipy.special import erf
+
+
+def gelu(x: np.ndarray) -> np.ndarray:
+    return 0.5 * x * (1.0 + erf(x / np.sqrt(2.0)).astype(x.dtype))
+
+
+def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float = 1e-5) -> np.ndarray:
+    mu = x.mean(-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(-1, keepdims=True)
+    return (x - mu) / np.sqrt(var + eps) * w + b
+
+
+def softmax(x: np.ndarray, axis: int = -1) -> np.ndarray:
+    m = x.max(axis=axis, keepdims=True)
+    e = np.exp(x - m)
+    return e / e.sum(axis=axis, keepdims=True)
+
+
+def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> np.ndarray:
+    """Encoder positional table (openai `sinusoids`; [TF] WhisperEncoder embed_positions init)."""
+    inc = np.log(max_timescale) / (channels // 2 - 1)
+    inv = np.exp(-inc * np.arange(channels // 2))
+    t = np.arange(length)[:, None] * inv[None, :]
+    return np.concatenate([np.sin(t), np.cos(t)], axis=1)
+
+
+def conv1d(x: np.ndarray, w: np.ndarray, b: np.ndarray, stride: int) -> np.ndarray:
+    """x [B, Cin, T], w [Cout, Cin, 3], padding 1 -> [B, Cout, T_out]."""
+    B, Cin, T = x.shape
+    xp = np.pad(x, ((0, 0), (0, 0), (1, 1)))
+    T_out = (T + 2 - 3) // stride + 1
+    cols = np.stack([xp[:, :, k: k + stride * (T_out - 1) + 1: stride] for k in range(3)], axis=-1)  # [B,Cin,Tout,3]
+    cols = cols.transpose(0, 2, 1, 3).reshape(B, T_out, Cin * 3)
+    y = cols @ w.reshape(w.shape[0], Cin * 3).T + b                                              # [B,Tout,Cout]
+    return y.transpose(0, 2, 1)
+
+
+class OracleWhisper:
+    def __init__(self, sd: Dict[str, np.ndarray], dims, dtype=np.float32):
+        self.dims = dims
+        self.dtype = dtype
+        self.w = {k: np.asarray(v, dtype=dtype) for k, v in sd.items()}
+        self.H = dims.n_head
+        self.hd = dims.n_state // dims.n_head
+
+    # ---------------------------------------------------------------- helpers
+    def _lin(self, x, name, bias=True):
+        y = x @ self.w[name + ".weight"].T
+        if bias and (name + ".bias") in self.w:
+            y = y + self.w[name + ".bias"]
+        return y
+
+    def _split(self, x):  # [B, T, d] -> [B, H, T, hd]
+        B, T, _ = x.shape
+        return x.reshape(B, T, self.H, self.hd).transpose(0, 2, 1, 3)
+
+    def _merge(self, x):  # [B, H, T, hd] -> [B, T, d]
+        B, H, T, hd = x.shape
+        return x.transpose(0, 2, 1, 3).reshape(B, T, H * hd)
+
+    def _attn(self, q, k, v, mask=None, return_weights=False):
+        s = (q @ k.transpose(0, 1, 3, 2)) / np.sqrt(self.hd).astype(self.dtype)
+        if mask is not None:
+            s = s + mask
+        p = softmax(s, -1)
+        o = p @ v
+        return (o, p) if return_weights else (o, None)
+
+    # ---------------------------------------------------------------- encoder
+    def encode(self, mel: np.ndarray) -> np.ndarray:
+        """mel [B, n_mels, 3000] -> [B, 1500, d]."""
+        w = self.w
+        x = np.asarray(mel, dtype=self.dtype)
+        x = gelu(conv1d(x, w["model.encoder.conv1.weight"], w["model.encoder.conv1.bias"], 1))
+        x = gelu(conv1d(x, w["model.encoder.conv2.weight"], w["model.encoder.conv2.bias"], 2))
+        x = x.transpose(0, 2, 1) + w["model.encoder.embed_positions.weight"][: x.shape[2]]
+        for i in range(self.dims.n_enc_layer):
+            p = f"model.encoder.layers.{i}."
+            h = layer_norm(x, w[p + "self_attn_layer_norm.weight"], w[p + "self_attn_layer_norm.bias"])
+            q = self._split(self._lin(h, p + "self_attn.q_proj"))
+            k = self._split(self._lin(h, p + "self_attn.k_proj", bias=False))
+            v = self._split(self._lin(h, p + "self_attn.v_proj"))
+            o, _ = self._attn(q, k, v)
+            x = x + self._lin(self._merge(o), p + "self_attn.out_proj")
+            h = layer_norm(x, w[p + "final_layer_norm.weight"], w[p + "final_layer_norm.bias"])
+            x = x + self._lin(gelu(self._lin(h, p + "fc1")), p + "fc2")
+        return layer_norm(x, w["model.encoder.layer_norm.weight"], w["model.encoder.layer_norm.bias"])
+
+    # ---------------------------------------------------------------- decoder
+    def cross_kv(self, enc: np.ndarray) -> List[Tuple[np.ndarray, np.ndarray]]:
+        out = []
+        enc = np.asarray(enc, dtype=self.dtype)
+        for i in range(self.dims.n_dec_layer):
+            p = f"model.decoder.layers.{i}.encoder_attn."
+            out.append((self._split(self._lin(enc, p + "k_proj", bias=False)), self._split(self._lin(enc, p + "v_proj"))))
+        return out
+
+    def decode(self, tokens: np.ndarray, cross: List[Tuple[np.ndarray, np.ndarray]],
+               cache: Optional[List[Tuple[np.ndarray, np.ndarray]]] = None, offset: int = 0,
+               return_cross_attn: bool = False):
+        """tokens [B, L] (positions offset..offset+L-1) -> (logits [B, L, V] float, new cache[, cross weights])."""
+        w = self.w
+        B, L = tokens.shape
+        x = w["model.decoder.embed_tokens.weight"][tokens] + w["model.decoder.embed_positions.weight"][offset: offset + L]
+        Ltot = offset + L
+        mask = np.triu(np.full((L, Ltot), -np.inf, dtype=self.dtype), k=offset + 1)
+        new_cache = []
+        cross_w = []
+        for i in range(self.dims.n_dec_layer):
+            p = f"model.decoder.layers.{i}."
+            h = layer_norm(x, w[p + "self_attn_layer_norm.weight"], w[p + "self_attn_layer_norm.bias"])
+            q = self._split(self._lin(h, p + "self_attn.q_proj"))
+            k = self._split(self._lin(h, p + "self_attn.k_proj", bias=False))
+            v = self._split(self._lin(h, p + "self_attn.v_proj"))
+            if cache is not None and offset > 0:
+                k = np.concatenate([cache[i][0], k], axis=2)
+                v = np.concatenate([cache[i][1], v], axis=2)
+            new_cache.append((k, v))
+            o, _ = self._attn(q, k, v, mask)
+            x = x + self._lin(self._merge(o), p + "self_attn.out_proj")
+            h = layer_norm(x, w[p + "encoder_attn_layer_norm.weight"], w[p + "encoder_attn_layer_norm.bias"])
+            q = self._split(self._lin(h, p + "encoder_attn.q_proj"))
+            ck, cv = cross[i]
+            if ck.shape[0] != B:        # hypotheses sharing one window's cross-KV (beam search)
+                rep = B // ck.shape[0]
+                ck, cv = np.repeat(ck, rep, axis=0), np.repeat(cv, rep, axis=0)
+            o, pw = self._attn(q, ck, cv, return_weights=return_cross_attn)
+            if return_cross_attn:
+                cross_w.append(pw)
+            x = x + self._lin(self._merge(o), p + "encoder_attn.out_proj")
+            h = layer_norm(x, w[p + "final_layer_norm.weight"], w[p + "final_layer_norm.bias"])
+            x = x + self._lin(gelu(self._lin(h, p + "fc1")), p + "fc2")
+        x = layer_norm(x, w["model.decoder.layer_norm.weight"], w["model.decoder.layer_norm.bias"])
+        logits = x @ w["model.decoder.embed_tokens.weight"].T
+        if return_cross_attn:
+            return logits, new_cache, cross_w
+        return logits, new_cache

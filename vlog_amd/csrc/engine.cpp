@@ -1,0 +1,781 @@
+// libwhisper_mi355 engine: C-ABI (include/whisper_mi355.h) over the gfx950 kernels.
+//
+// Owns: the packed bf16/f32 weight arena, the encoder scratch, the decoder state (cross-KV slots, self-KV
+// cache, token/lineage tables) and the decode loop.  Orchestration mirrors what CTranslate2's
+// models::Whisper does below faster-whisper [FW↑] (encode -> generate with logit rules -> results), but the
+// loop keeps everything on the device: per step one decoder pass (embed, L x {LN, QKV GEMM -> KV cache,
+// self-attn, O GEMM+residual, LN, Q GEMM, cross-attn, O GEMM+residual, LN, FC1+GELU, FC2+residual}, final
+// LN, tied-embedding logits GEMM) and one selection kernel; the host only polls an "active hypotheses"
+// counter every `check_every` steps.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/whisper_mi355.h"
+#include "gemm.h"
+#include "search.h"
+
+// ---- launchers defined in the .hip files
+void launch_logmel(const float*, long long, long long, long long, long long, int, const float*, const float*,
+                   const float*, const float*, const int*, const int*, int, float*, long long, unsigned int*, hipStream_t);
+void launch_logmel_clamp(float*, long long, long long, long long, const unsigned int*, const float*, hipStream_t);
+void launch_ordered_to_float(const unsigned int*, float*, hipStream_t);
+void launch_layernorm(const float*, long long, const int*, int, int, const float*, const float*, bf16*, long long, hipStream_t);
+void launch_embed(const int*, const int*, const bf16*, const float*, float*, int, int, hipStream_t);
+void launch_im2col_conv1(const float*, long long, const int*, const int*, int, int, int, bf16*, hipStream_t);
+void launch_zero_pad_rows(bf16*, int, long long, int, hipStream_t);
+void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
+void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const int*, const int*, const int*, const int*,
+                      bf16*, long long, int, int, int, hipStream_t);
+void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
+                       long long, int, int, int, float*, float*, float*, float*, const int*, int, hipStream_t);
+
+namespace {
+
+thread_local std::string g_err;
+
+#define HIP_OK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e__ = (x);                                                                          \
+    if (e__ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e__)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) HIP_OK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    HIP_OK(hipMalloc(&p, b));
+    bytes = b;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+struct Slot {
+  size_t off, bytes;
+  bool set = false;
+};
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+struct wm_engine {
+  wm_model_dims dm;
+  int device;
+  std::mutex mu;
+  // weights
+  std::map<std::string, Slot> slots;
+  DevBuf arena;
+  int k1p;  // padded conv1 K
+  // frontend constants
+  DevBuf fe_window, fe_cos, fe_sin, fe_filt, fe_lo, fe_hi;
+  // encoder scratch
+  DevBuf e_cols, e_h1, e_x, e_hb, e_qkv, e_ao, e_ff, e_seek, e_len;
+  int enc_cap = 0;
+  // decoder state
+  int n_slots = 0, n_hyp_cap = 0;
+  DevBuf ckv, skv;
+  DevBuf d_tokens, d_lin, d_seq_len, d_done, d_cum, d_row_tok, d_row_pos, d_row_hyp, d_hyp_slot, d_n_active;
+  DevBuf d_suppress, d_cand_tok, d_cand_lp, d_fin_tok, d_fin_len, d_fin_cum, d_n_fin, d_ns, d_logit_rows;
+  DevBuf d_prow_tok, d_prow_pos, d_prow_hyp, d_head_map;
+  // step activations
+  DevBuf s_x, s_hb, s_q, s_ao, s_ff, s_logits, s_pm, s_pl, s_po;
+
+  const Slot& slot(const std::string& n) const {
+    auto it = slots.find(n);
+    if (it == slots.end()) throw std::runtime_error("unknown weight " + n);
+    return it->second;
+  }
+  template <class T> T* W(const std::string& n) const { return (T*)((char*)arena.p + slot(n).off); }
+  const bf16* Wb(const std::string& n) const { return W<bf16>(n); }
+  const float* Wf(const std::string& n) const { return W<float>(n); }
+
+  size_t device_bytes() const {
+    size_t t = arena.bytes;
+    for (const DevBuf* b : {&e_cols, &e_h1, &e_x, &e_hb, &e_qkv, &e_ao, &e_ff, &ckv, &skv, &s_x, &s_hb, &s_q, &s_ao,
+                            &s_ff, &s_logits, &s_pm, &s_pl, &s_po, &d_tokens, &d_lin, &d_fin_tok})
+      t += b->bytes;
+    return t;
+  }
+};
+
+namespace {
+
+void add_slot(wm_engine* e, size_t& off, const std::string& name, size_t bytes) {
+  e->slots[name] = Slot{off, bytes, false};
+  off += align256(bytes);
+}
+
+void build_layout(wm_engine* e) {
+  const auto& m = e->dm;
+  const size_t d = m.n_state, f = 4 * d, b2 = 2, f4 = 4;
+  e->k1p = ((3 * m.n_mels + 63) / 64) * 64;
+  size_t off = 0;
+  add_slot(e, off, "enc.conv1.w", d * e->k1p * b2);
+  add_slot(e, off, "enc.conv1.b", d * f4);
+  add_slot(e, off, "enc.conv2.w", d * 3 * d * b2);
+  add_slot(e, off, "enc.conv2.b", d * f4);
+  add_slot(e, off, "enc.pos", (size_t)m.n_audio_ctx * d * f4);
+  for (int l = 0; l < m.n_enc_layer; ++l) {
+    const std::string p = "enc." + std::to_string(l) + ".";
+    add_slot(e, off, p + "ln1.w", d * f4); add_slot(e, off, p + "ln1.b", d * f4);
+    add_slot(e, off, p + "qkv.w", 3 * d * d * b2); add_slot(e, off, p + "qkv.b", 3 * d * f4);
+    add_slot(e, off, p + "out.w", d * d * b2); add_slot(e, off, p + "out.b", d * f4);
+    add_slot(e, off, p + "ln2.w", d * f4); add_slot(e, off, p + "ln2.b", d * f4);
+    add_slot(e, off, p + "fc1.w", f * d * b2); add_slot(e, off, p + "fc1.b", f * f4);
+    add_slot(e, off, p + "fc2.w", d * f * b2); add_slot(e, off, p + "fc2.b", d * f4);
+  }
+  add_slot(e, off, "enc.ln.w", d * f4); add_slot(e, off, "enc.ln.b", d * f4);
+  add_slot(e, off, "dec.embed", (size_t)m.n_vocab * d * b2);
+  add_slot(e, off, "dec.pos", (size_t)m.n_text_ctx * d * f4);
+  for (int l = 0; l < m.n_dec_layer; ++l) {
+    const std::string p = "dec." + std::to_string(l) + ".";
+    add_slot(e, off, p + "ln1.w", d * f4); add_slot(e, off, p + "ln1.b", d * f4);
+    add_slot(e, off, p + "qkv.w", 3 * d * d * b2); add_slot(e, off, p + "qkv.b", 3 * d * f4);
+    add_slot(e, off, p + "out.w", d * d * b2); add_slot(e, off, p + "out.b", d * f4);
+    add_slot(e, off, p + "ln2.w", d * f4); add_slot(e, off, p + "ln2.b", d * f4);
+    add_slot(e, off, p + "cq.w", d * d * b2); add_slot(e, off, p + "cq.b", d * f4);
+    add_slot(e, off, p + "cout.w", d * d * b2); add_slot(e, off, p + "cout.b", d * f4);
+    add_slot(e, off, p + "ln3.w", d * f4); add_slot(e, off, p + "ln3.b", d * f4);
+    add_slot(e, off, p + "fc1.w", f * d * b2); add_slot(e, off, p + "fc1.b", f * f4);
+    add_slot(e, off, p + "fc2.w", d * f * b2); add_slot(e, off, p + "fc2.b", d * f4);
+  }
+  add_slot(e, off, "dec.ckv.w", (size_t)m.n_dec_layer * 2 * d * d * b2);
+  add_slot(e, off, "dec.ckv.b", (size_t)m.n_dec_layer * 2 * d * f4);
+  add_slot(e, off, "dec.ln.w", d * f4); add_slot(e, off, "dec.ln.b", d * f4);
+  e->arena.ensure(off);
+}
+
+// slaney mel filterbank (faster-whisper get_mel_filters), periodic Hann, DFT twiddles — host f64 -> f32
+void build_frontend(wm_engine* e, hipStream_t st) {
+  const int nm = e->dm.n_mels, nb = 201, nfft = 400, sr = 16000;
+  std::vector<float> win(nfft), c(nfft), s(nfft);
+  for (int n = 0; n < nfft; ++n) {
+    win[n] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * n / nfft));
+    c[n] = (float)std::cos(2.0 * M_PI * n / nfft);
+    s[n] = (float)std::sin(2.0 * M_PI * n / nfft);
+  }
+  std::vector<double> mels(nm + 2), freqs(nm + 2), fft(nb);
+  const double max_mel = 45.245640471924965, f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp;
+  const double logstep = std::log(6.4) / 27.0;
+  for (int i = 0; i < nm + 2; ++i) {
+    mels[i] = max_mel * i / (nm + 1);
+    freqs[i] = mels[i] >= min_log_mel ? min_log_hz * std::exp(logstep * (mels[i] - min_log_mel)) : f_sp * mels[i];
+  }
+  for (int k = 0; k < nb; ++k) fft[k] = (double)k * sr / nfft;
+  std::vector<float> filt((size_t)nm * nb, 0.f);
+  std::vector<int> lo(nm, nb), hi(nm, 0);
+  for (int m = 0; m < nm; ++m) {
+    const double enorm = 2.0 / (freqs[m + 2] - freqs[m]);
+    for (int k = 0; k < nb; ++k) {
+      const double lower = -(freqs[m] - fft[k]) / (freqs[m + 1] - freqs[m]);
+      const double upper = (freqs[m + 2] - fft[k]) / (freqs[m + 2] - freqs[m + 1]);
+      const double w = std::max(0.0, std::min(lower, upper)) * enorm;
+      filt[(size_t)m * nb + k] = (float)w;
+      if (w > 0) { lo[m] = std::min(lo[m], k); hi[m] = std::max(hi[m], k + 1); }
+    }
+    if (lo[m] >= hi[m]) { lo[m] = 0; hi[m] = 0; }
+  }
+  auto up = [&](DevBuf& b, const void* src, size_t bytes) {
+    b.ensure(bytes);
+    HIP_OK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, st));
+  };
+  up(e->fe_window, win.data(), nfft * 4);
+  up(e->fe_cos, c.data(), nfft * 4);
+  up(e->fe_sin, s.data(), nfft * 4);
+  up(e->fe_filt, filt.data(), filt.size() * 4);
+  up(e->fe_lo, lo.data(), nm * 4);
+  up(e->fe_hi, hi.data(), nm * 4);
+  HIP_OK(hipStreamSynchronize(st));
+}
+
+GemmEpi epi_of(int kind, void* out, long long ldc, const float* bias) {
+  GemmEpi p;
+  std::memset(&p, 0, sizeof(p));
+  p.kind = kind;
+  p.out = out;
+  p.ldc = ldc;
+  p.bias = bias;
+  return p;
+}
+GemmA amat(const bf16* ptr, long long ld) { return GemmA{ptr, ld, 0, 0}; }
+
+// ------------------------------------------------------------------------------------------ encoder
+void encode_chunk(wm_engine* e, const float* mel, long long ld, const int* h_seek, const int* h_len, int B, bf16* out,
+                  hipStream_t st) {
+  const auto& m = e->dm;
+  const int d = m.n_state, T = m.n_audio_ctx, L = m.n_enc_layer, H = m.n_head;
+  const long long M = (long long)B * T;
+  if (B > e->enc_cap) {
+    e->e_cols.ensure((size_t)B * 3000 * e->k1p * 2);
+    e->e_h1.ensure((size_t)B * 3001 * d * 2);
+    e->e_x.ensure((size_t)M * d * 4);
+    e->e_hb.ensure((size_t)M * d * 2);
+    e->e_qkv.ensure((size_t)M * 3 * d * 2);
+    e->e_ao.ensure((size_t)M * d * 2);
+    e->e_ff.ensure((size_t)M * 4 * d * 2);
+    e->e_seek.ensure(B * 4);
+    e->e_len.ensure(B * 4);
+    e->enc_cap = B;
+  }
+  HIP_OK(hipMemcpyAsync(e->e_seek.p, h_seek, B * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->e_len.p, h_len, B * 4, hipMemcpyHostToDevice, st));
+  bf16* cols = e->e_cols.as<bf16>();
+  bf16* h1 = e->e_h1.as<bf16>();
+  float* x = e->e_x.as<float>();
+  bf16* hb = e->e_hb.as<bf16>();
+  bf16* qkv = e->e_qkv.as<bf16>();
+  bf16* ao = e->e_ao.as<bf16>();
+  bf16* ff = e->e_ff.as<bf16>();
+  // conv1 (implicit GEMM over the window-sliced mel) + GELU -> h1 rows 1..3000 of each [3001][d] block
+  launch_im2col_conv1(mel, ld, e->e_seek.as<int>(), e->e_len.as<int>(), B, m.n_mels, e->k1p, cols, st);
+  launch_zero_pad_rows(h1, B, 3001LL * d, d, st);
+  {
+    GemmEpi ep = epi_of(EPI_BF16, h1, d, e->Wf("enc.conv1.b"));
+    ep.act = 1; ep.rpb = 3000; ep.bstride = 3001LL * d; ep.roff = 1;
+    launch_gemm(amat(cols, e->k1p), e->Wb("enc.conv1.w"), e->k1p, B * 3000, d, e->k1p, ep, st);
+  }
+  // conv2 (k3, s2): row t of window b reads h1 rows 2t-1, 2t, 2t+1 = 3d contiguous elements starting at
+  // block row 2t (the zero row 0 is the left padding); + GELU + positional embedding -> residual x
+  {
+    GemmA a{h1, 2LL * d, T, 3001LL * d};
+    GemmEpi ep = epi_of(EPI_GELU_POS_F32, x, d, e->Wf("enc.conv2.b"));
+    ep.rpb = T; ep.pos = e->Wf("enc.pos");
+    launch_gemm(a, e->Wb("enc.conv2.w"), 3LL * d, (int)M, d, 3 * d, ep, st);
+  }
+  for (int l = 0; l < L; ++l) {
+    const std::string p = "enc." + std::to_string(l) + ".";
+    launch_layernorm(x, d, nullptr, (int)M, d, e->Wf(p + "ln1.w"), e->Wf(p + "ln1.b"), hb, d, st);
+    launch_gemm(amat(hb, d), e->Wb(p + "qkv.w"), d, (int)M, 3 * d, d, epi_of(EPI_BF16, qkv, 3LL * d, e->Wf(p + "qkv.b")), st);
+    launch_attn_enc(qkv, ao, B, T, d, H, st);
+    launch_gemm(amat(ao, d), e->Wb(p + "out.w"), d, (int)M, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
+    launch_layernorm(x, d, nullptr, (int)M, d, e->Wf(p + "ln2.w"), e->Wf(p + "ln2.b"), hb, d, st);
+    {
+      GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, e->Wf(p + "fc1.b"));
+      ep.act = 1;
+      launch_gemm(amat(hb, d), e->Wb(p + "fc1.w"), d, (int)M, 4 * d, d, ep, st);
+    }
+    launch_gemm(amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, (int)M, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
+  }
+  launch_layernorm(x, d, nullptr, (int)M, d, e->Wf("enc.ln.w"), e->Wf("enc.ln.b"), out, d, st);
+}
+
+// ------------------------------------------------------------------------------------------ decoder
+void ensure_step(wm_engine* e, int rows, int logit_rows) {
+  const int d = e->dm.n_state, H = e->dm.n_head;
+  e->s_x.ensure((size_t)rows * d * 4);
+  e->s_hb.ensure((size_t)rows * d * 2);
+  e->s_q.ensure((size_t)rows * d * 2);
+  e->s_ao.ensure((size_t)rows * d * 2);
+  e->s_ff.ensure((size_t)rows * 4 * d * 2);
+  e->s_logits.ensure((size_t)logit_rows * e->dm.n_vocab * 4);
+  e->s_pm.ensure((size_t)rows * H * 16 * 4);
+  e->s_pl.ensure((size_t)rows * H * 16 * 4);
+  e->s_po.ensure((size_t)rows * H * 16 * 64 * 4);
+  e->d_prow_tok.ensure((size_t)rows * 4);
+  e->d_prow_pos.ensure((size_t)rows * 4);
+  e->d_prow_hyp.ensure((size_t)rows * 4);
+  e->d_logit_rows.ensure((size_t)logit_rows * 4);
+}
+
+int cross_splits(int rows, int H) {
+  int pairs = rows * H;
+  int s = (2048 + pairs - 1) / pairs;
+  if (s < 1) s = 1;
+  if (s > 16) s = 16;
+  return s;
+}
+
+// One decoder pass over `rows` rows; logits for the n_logit rows listed in logit_rows (device) go to
+// `logits`.  Optional cross-attention capture (align): head_map per layer computed by caller.
+void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos, const int* row_hyp, const int* done,
+                  const int* lin, const int* logit_rows, int n_logit, float* logits,
+                  const std::vector<std::vector<int>>* align_map, int n_align, float* attn, hipStream_t st) {
+  const auto& m = e->dm;
+  const int d = m.n_state, H = m.n_head, L = m.n_dec_layer, T = m.n_audio_ctx, C = m.n_text_ctx;
+  float* x = e->s_x.as<float>();
+  bf16* hb = e->s_hb.as<bf16>();
+  bf16* q = e->s_q.as<bf16>();
+  bf16* ao = e->s_ao.as<bf16>();
+  bf16* ff = e->s_ff.as<bf16>();
+  const size_t skv_layer = (size_t)e->n_hyp_cap * H * C * 64;      // elements per (layer, k|v)
+  const size_t ckv_layer = (size_t)e->n_slots * H * T * 64;
+  bf16* skv = e->skv.as<bf16>();
+  bf16* ckv = e->ckv.as<bf16>();
+  const int splits = attn ? 1 : cross_splits(rows, H);
+  launch_embed(row_tok, row_pos, e->Wb("dec.embed"), e->Wf("dec.pos"), x, rows, d, st);
+  for (int l = 0; l < L; ++l) {
+    const std::string p = "dec." + std::to_string(l) + ".";
+    bf16* kc = skv + (size_t)(2 * l) * skv_layer;
+    bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
+    launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln1.w"), e->Wf(p + "ln1.b"), hb, d, st);
+    {
+      GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, e->Wf(p + "qkv.b"));
+      ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
+      ep.d = d; ep.n_head = H; ep.head_dim = 64; ep.n_ctx = C;
+      launch_gemm(amat(hb, d), e->Wb(p + "qkv.w"), d, rows, 3 * d, d, ep, st);
+    }
+    launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, st);
+    launch_gemm(amat(ao, d), e->Wb(p + "out.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
+    launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln2.w"), e->Wf(p + "ln2.b"), hb, d, st);
+    launch_gemm(amat(hb, d), e->Wb(p + "cq.w"), d, rows, d, d, epi_of(EPI_BF16, q, d, e->Wf(p + "cq.b")), st);
+    float* probs = nullptr;
+    const int* hmap = nullptr;
+    if (attn && align_map) {
+      const auto& mp = (*align_map)[l];
+      bool any = false;
+      for (int v : mp) any |= v >= 0;
+      if (any) {
+        HIP_OK(hipMemcpyAsync(e->d_head_map.p, mp.data(), H * 4, hipMemcpyHostToDevice, st));
+        probs = attn;
+        hmap = e->d_head_map.as<int>();
+      }
+    }
+    launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
+                      e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, splits, e->s_pm.as<float>(),
+                      e->s_pl.as<float>(), e->s_po.as<float>(), probs, hmap, n_align, st);
+    if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
+    launch_gemm(amat(ao, d), e->Wb(p + "cout.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "cout.b")), st);
+    launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln3.w"), e->Wf(p + "ln3.b"), hb, d, st);
+    {
+      GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, e->Wf(p + "fc1.b"));
+      ep.act = 1;
+      launch_gemm(amat(hb, d), e->Wb(p + "fc1.w"), d, rows, 4 * d, d, ep, st);
+    }
+    launch_gemm(amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
+  }
+  launch_layernorm(x, d, logit_rows, n_logit, d, e->Wf("dec.ln.w"), e->Wf("dec.ln.b"), hb, d, st);
+  launch_gemm(amat(hb, d), e->Wb("dec.embed"), d, n_logit, m.n_vocab, d, epi_of(EPI_F32, logits, m.n_vocab, nullptr), st);
+}
+
+void check_weights(wm_engine* e) {
+  for (auto& kv : e->slots)
+    if (!kv.second.set) throw std::runtime_error("weight not set: " + kv.first);
+}
+
+void reserve(wm_engine* e, int n_slots, int n_hyp) {
+  const auto& m = e->dm;
+  const int H = m.n_head, C = m.n_text_ctx, T = m.n_audio_ctx, L = m.n_dec_layer;
+  if (n_slots > e->n_slots) {
+    DevBuf nb;
+    nb.ensure((size_t)L * 2 * n_slots * H * T * 64 * 2);
+    e->ckv.release();
+    e->ckv = nb;
+    e->n_slots = n_slots;
+  }
+  if (n_hyp > e->n_hyp_cap) {
+    e->skv.release();
+    e->skv.ensure((size_t)L * 2 * n_hyp * H * C * 64 * 2);
+    e->n_hyp_cap = n_hyp;
+    const size_t nh = n_hyp;
+    e->d_tokens.ensure(nh * C * 4);
+    e->d_lin.ensure(nh * C * 4);
+    e->d_seq_len.ensure(nh * 4);
+    e->d_done.ensure(nh * 4);
+    e->d_cum.ensure(nh * 4);
+    e->d_row_tok.ensure(nh * 4);
+    e->d_row_pos.ensure(nh * 4);
+    e->d_row_hyp.ensure(nh * 4);
+    e->d_hyp_slot.ensure(nh * 4);
+    e->d_cand_tok.ensure(nh * 9 * 4);
+    e->d_cand_lp.ensure(nh * 9 * 4);
+    e->d_ns.ensure(nh * 4);
+    e->d_fin_tok.ensure(nh * 16 * C * 4);
+    e->d_fin_len.ensure(nh * 16 * 4);
+    e->d_fin_cum.ensure(nh * 16 * 4);
+    e->d_n_fin.ensure(nh * 4);
+  }
+  e->d_n_active.ensure(4);
+  e->d_suppress.ensure((size_t)m.n_vocab);
+  e->d_head_map.ensure((size_t)H * 4);
+}
+
+void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
+  check_weights(e);
+  const auto& m = e->dm;
+  const int C = m.n_text_ctx, V = m.n_vocab;
+  const int W = a->n_windows, P = a->prompt_len;
+  if (W <= 0) return;
+  if (P <= 0 || P >= a->max_length || a->max_length > C) throw std::runtime_error("generate: bad prompt_len/max_length");
+  const bool beam = a->beam_size > 1 && a->temperature <= 0.f;
+  const bool sampling = a->temperature > 0.f;
+  const int per = beam ? a->beam_size : (sampling ? std::max(1, a->num_hypotheses) : 1);
+  const int NH = W * per;
+  if (beam && a->beam_size > 8) throw std::runtime_error("generate: beam_size <= 8 supported");
+  for (int w = 0; w < W; ++w)
+    if (a->h_slots[w] < 0 || a->h_slots[w] >= e->n_slots) throw std::runtime_error("generate: slot out of range");
+  reserve(e, e->n_slots, NH);
+  const int max_cand = beam ? std::max(1, (int)std::lround(a->beam_size * a->patience)) : 0;
+  if (max_cand > 16) throw std::runtime_error("generate: beam_size * patience must be <= 16");
+
+  // ---- host-side init of the state tables
+  std::vector<int> tokens((size_t)NH * C, 0), lin((size_t)NH * C, 0), seq_len(NH, P), zeros(NH, 0), hyp_slot(NH);
+  std::vector<float> cum(NH, 0.f);
+  for (int h = 0; h < NH; ++h) {
+    const int w = h / per;
+    hyp_slot[h] = a->h_slots[w];
+    for (int p = 0; p < P; ++p) tokens[(size_t)h * C + p] = a->h_prompts[(size_t)w * P + p];
+    for (int p = 0; p < C; ++p) lin[(size_t)h * C + p] = h;
+    if (beam && (h % per) != 0) cum[h] = -INFINITY;
+  }
+  std::vector<unsigned char> sup(V, 0);
+  for (int i = 0; i < a->n_suppress; ++i)
+    if (a->h_suppress[i] >= 0 && a->h_suppress[i] < V) sup[a->h_suppress[i]] = 1;
+  HIP_OK(hipMemcpyAsync(e->d_tokens.p, tokens.data(), tokens.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_lin.p, lin.data(), lin.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_seq_len.p, seq_len.data(), NH * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_done.p, zeros.data(), NH * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_n_fin.p, zeros.data(), NH * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_cum.p, cum.data(), NH * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_hyp_slot.p, hyp_slot.data(), NH * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_suppress.p, sup.data(), V, hipMemcpyHostToDevice, st));
+  int n_active = NH;
+  HIP_OK(hipMemcpyAsync(e->d_n_active.p, &n_active, 4, hipMemcpyHostToDevice, st));
+
+  // ---- prefill: rows (h, p) for every prompt position
+  const int rows = NH * P;
+  const int nlog = a->sot_index >= 0 ? 2 * NH : NH;
+  ensure_step(e, std::max(rows, NH), std::max(nlog, NH));
+  {
+    std::vector<int> rt(rows), rp(rows), rh(rows), lr(nlog);
+    for (int h = 0; h < NH; ++h)
+      for (int p = 0; p < P; ++p) {
+        const int r = h * P + p;
+        rt[r] = tokens[(size_t)h * C + p]; rp[r] = p; rh[r] = h;
+      }
+    for (int h = 0; h < NH; ++h) {
+      lr[h] = h * P + P - 1;
+      if (a->sot_index >= 0) lr[NH + h] = h * P + a->sot_index;
+    }
+    HIP_OK(hipMemcpyAsync(e->d_prow_tok.p, rt.data(), rows * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(e->d_prow_pos.p, rp.data(), rows * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(e->d_prow_hyp.p, rh.data(), rows * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(e->d_logit_rows.p, lr.data(), nlog * 4, hipMemcpyHostToDevice, st));
+    std::vector<int> ident(NH);
+    for (int h = 0; h < NH; ++h) ident[h] = h;
+    HIP_OK(hipMemcpyAsync(e->d_row_hyp.p, ident.data(), NH * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));   // host vectors above go out of scope
+  }
+  float* logits = e->s_logits.as<float>();
+  decoder_pass(e, rows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_prow_hyp.as<int>(), nullptr,
+               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, logits, nullptr, 0, nullptr, st);
+  if (a->sot_index >= 0) launch_no_speech(logits + (size_t)NH * V, V, V, NH, m.no_speech, e->d_ns.as<float>(), st);
+
+  SearchParams sp;
+  std::memset(&sp, 0, sizeof(sp));
+  sp.logits = logits; sp.ldl = V; sp.V = V;
+  sp.tokens = e->d_tokens.as<int>(); sp.n_ctx = C; sp.seq_len = e->d_seq_len.as<int>(); sp.sample_begin = P;
+  sp.suppress = e->d_suppress.as<unsigned char>(); sp.suppress_blank = a->suppress_blank; sp.blank = m.blank;
+  sp.eot = m.eot; sp.no_timestamps = m.no_timestamps; sp.ts_begin = m.timestamp_begin;
+  sp.max_initial = a->max_initial_timestamp_index; sp.with_ts = a->with_timestamps; sp.done = e->d_done.as<int>();
+  sp.mode = beam ? 1 : (sampling ? 2 : 0); sp.topk = beam ? a->beam_size + 1 : 1;
+  sp.inv_temperature = sampling ? 1.0f / a->temperature : 1.0f; sp.seed = a->seed; sp.max_length = a->max_length;
+  sp.cum = e->d_cum.as<float>(); sp.row_tok = e->d_row_tok.as<int>(); sp.row_pos = e->d_row_pos.as<int>();
+  sp.n_active = e->d_n_active.as<int>(); sp.cand_tok = e->d_cand_tok.as<int>(); sp.cand_lp = e->d_cand_lp.as<float>();
+  BeamParams bp;
+  std::memset(&bp, 0, sizeof(bp));
+  bp.beam = a->beam_size; bp.max_cand = max_cand; bp.n_ctx = C; bp.sample_begin = P; bp.max_length = a->max_length;
+  bp.eot = m.eot; bp.cand_tok = sp.cand_tok; bp.cand_lp = sp.cand_lp; bp.tokens = sp.tokens; bp.lin = e->d_lin.as<int>();
+  bp.seq_len = sp.seq_len; bp.cum = sp.cum; bp.done = sp.done; bp.row_tok = sp.row_tok; bp.row_pos = sp.row_pos;
+  bp.fin_tok = e->d_fin_tok.as<int>(); bp.fin_len = e->d_fin_len.as<int>(); bp.fin_cum = e->d_fin_cum.as<float>();
+  bp.n_fin = e->d_n_fin.as<int>(); bp.n_active = sp.n_active;
+
+  auto select = [&](int step) {
+    sp.step = step;
+    launch_logits_select(sp, NH, st);
+    if (beam) launch_beam_select(bp, W, st);
+  };
+  select(0);
+  int steps = 1;
+  const int max_steps = a->max_length - P;      // generated tokens (incl. the final one) <= max_length - P
+  const int check = std::max(1, a->check_every);
+  for (int step = 1; step < max_steps; ++step) {
+    if ((step - 1) % check == 0) {
+      int act = 0;
+      HIP_OK(hipMemcpyAsync(&act, e->d_n_active.p, 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      if (act <= 0) break;
+    }
+    // logits rows of a decode step are the hypotheses themselves
+    decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
+                 e->d_lin.as<int>(), e->d_row_hyp.as<int>(), NH, logits, nullptr, 0, nullptr, st);
+    select(step);
+    ++steps;
+  }
+
+  // ---- results
+  std::vector<int> out_tok((size_t)NH * C), out_len(NH);
+  std::vector<float> out_cum(NH), ns(NH, 0.f);
+  HIP_OK(hipMemcpyAsync(out_tok.data(), e->d_tokens.p, out_tok.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(out_len.data(), e->d_seq_len.p, NH * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(out_cum.data(), e->d_cum.p, NH * 4, hipMemcpyDeviceToHost, st));
+  if (a->sot_index >= 0) HIP_OK(hipMemcpyAsync(ns.data(), e->d_ns.p, NH * 4, hipMemcpyDeviceToHost, st));
+  std::vector<int> fin_tok, fin_len, n_fin;
+  std::vector<float> fin_cum;
+  if (beam) {
+    fin_tok.resize((size_t)W * max_cand * C); fin_len.resize((size_t)W * max_cand); fin_cum.resize((size_t)W * max_cand);
+    n_fin.resize(W);
+    HIP_OK(hipMemcpyAsync(fin_tok.data(), e->d_fin_tok.p, fin_tok.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(fin_len.data(), e->d_fin_len.p, fin_len.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(fin_cum.data(), e->d_fin_cum.p, fin_cum.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(n_fin.data(), e->d_n_fin.p, W * 4, hipMemcpyDeviceToHost, st));
+  }
+  HIP_OK(hipStreamSynchronize(st));
+  const float lp = a->length_penalty;
+  auto norm = [&](float c, int n) { return c / std::pow((float)std::max(n, 1), lp); };
+  for (int w = 0; w < W; ++w) {
+    const int ML = a->max_length;
+    int best_len = 0;
+    float best_cum = 0.f, best_score = -INFINITY;
+    const int* best_ptr = nullptr;
+    if (beam) {
+      struct C2 { const int* t; int n; float c; };
+      std::vector<C2> cands;
+      for (int i = 0; i < n_fin[w]; ++i)
+        cands.push_back({&fin_tok[((size_t)w * max_cand + i) * C], fin_len[(size_t)w * max_cand + i], fin_cum[(size_t)w * max_cand + i]});
+      if ((int)cands.size() < a->beam_size) {       // openai finalize: add unfinished beams by sum_logprob
+        std::vector<int> order;
+        for (int b = 0; b < per; ++b)
+          if (out_cum[w * per + b] > -INFINITY) order.push_back(b);
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return out_cum[w * per + x] > out_cum[w * per + y]; });
+        for (int b : order) {
+          if ((int)cands.size() >= a->beam_size) break;
+          const int h = w * per + b;
+          cands.push_back({&out_tok[(size_t)h * C + P], out_len[h] - P, out_cum[h]});
+        }
+      }
+      for (const auto& c : cands) {
+        const float s = norm(c.c, c.n);
+        if (s > best_score) { best_score = s; best_len = c.n; best_cum = c.c; best_ptr = c.t; }
+      }
+    } else {
+      for (int j = 0; j < per; ++j) {
+        const int h = w * per + j;
+        const int n = out_len[h] - P;
+        const float s = norm(out_cum[h], n);
+        if (s > best_score) { best_score = s; best_len = n; best_cum = out_cum[h]; best_ptr = &out_tok[(size_t)h * C + P]; }
+      }
+    }
+    for (int i = 0; i < best_len && i < ML; ++i) a->h_tokens[(size_t)w * ML + i] = best_ptr[i];
+    a->h_lengths[w] = best_len;
+    a->h_scores[w] = best_score;
+    if (a->h_cum_logprob) a->h_cum_logprob[w] = best_cum;
+    if (a->h_no_speech) a->h_no_speech[w] = ns[w * per];
+  }
+  if (a->h_steps) a->h_steps[0] = steps;
+}
+
+void forward(wm_engine* e, int n_seq, const int* h_slots, int S, const int* h_tokens, float* d_logits, int last_only,
+             const int* h_align, int n_align, float* d_attn, hipStream_t st) {
+  check_weights(e);
+  const auto& m = e->dm;
+  const int C = m.n_text_ctx, H = m.n_head;
+  if (S <= 0 || S > C) throw std::runtime_error("forward: bad seq_len");
+  reserve(e, e->n_slots, n_seq);
+  const int rows = n_seq * S;
+  const int nlog = last_only ? n_seq : rows;
+  ensure_step(e, rows, 1);
+  std::vector<int> rt(rows), rp(rows), rh(rows), lr(nlog), hs(n_seq), lin((size_t)n_seq * C);
+  for (int s = 0; s < n_seq; ++s) {
+    if (h_slots[s] < 0 || h_slots[s] >= e->n_slots) throw std::runtime_error("forward: slot out of range");
+    hs[s] = h_slots[s];
+    for (int p = 0; p < S; ++p) {
+      const int r = s * S + p;
+      rt[r] = h_tokens[r]; rp[r] = p; rh[r] = s;
+    }
+    for (int p = 0; p < C; ++p) lin[(size_t)s * C + p] = s;
+  }
+  for (int i = 0; i < nlog; ++i) lr[i] = last_only ? i * S + S - 1 : i;
+  std::vector<std::vector<int>> amap(m.n_dec_layer, std::vector<int>(H, -1));
+  for (int i = 0; i < n_align; ++i) {
+    const int l = h_align[2 * i], h = h_align[2 * i + 1];
+    if (l < 0 || l >= m.n_dec_layer || h < 0 || h >= H) throw std::runtime_error("forward: bad alignment head");
+    amap[l][h] = i;
+  }
+  e->d_logit_rows.ensure((size_t)nlog * 4);
+  HIP_OK(hipMemcpyAsync(e->d_prow_tok.p, rt.data(), rows * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_prow_pos.p, rp.data(), rows * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_prow_hyp.p, rh.data(), rows * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_logit_rows.p, lr.data(), nlog * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_hyp_slot.p, hs.data(), n_seq * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_lin.p, lin.data(), lin.size() * 4, hipMemcpyHostToDevice, st));
+  decoder_pass(e, rows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_prow_hyp.as<int>(), nullptr,
+               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, d_logits, n_align ? &amap : nullptr, n_align,
+               n_align ? d_attn : nullptr, st);
+  HIP_OK(hipStreamSynchronize(st));
+}
+
+template <class F>
+int guarded(wm_engine* e, F&& f) {
+  try {
+    if (!e) throw std::runtime_error("null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    f();
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* wm_last_error(void) { return g_err.c_str(); }
+int32_t wm_abi_version(void) { return 1; }
+
+int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
+  try {
+    if (!dims || !out) throw std::runtime_error("wm_create: null argument");
+    if (dims->n_state % 64 != 0 || dims->n_state / dims->n_head != 64)
+      throw std::runtime_error("wm_create: head_dim must be 64 and n_state a multiple of 64");
+    if (dims->n_audio_ctx != 1500) throw std::runtime_error("wm_create: n_audio_ctx must be 1500");
+    HIP_OK(hipSetDevice(device));
+    auto* e = new wm_engine();
+    e->dm = *dims;
+    e->device = device;
+    try {
+      build_layout(e);
+      build_frontend(e, nullptr);
+    } catch (...) {
+      delete e;
+      throw;
+    }
+    *out = e;
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+void wm_destroy(wm_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  for (DevBuf* b : {&e->arena, &e->fe_window, &e->fe_cos, &e->fe_sin, &e->fe_filt, &e->fe_lo, &e->fe_hi, &e->e_cols,
+                    &e->e_h1, &e->e_x, &e->e_hb, &e->e_qkv, &e->e_ao, &e->e_ff, &e->e_seek, &e->e_len, &e->ckv,
+                    &e->skv, &e->d_tokens, &e->d_lin, &e->d_seq_len, &e->d_done, &e->d_cum, &e->d_row_tok,
+                    &e->d_row_pos, &e->d_row_hyp, &e->d_hyp_slot, &e->d_n_active, &e->d_suppress, &e->d_cand_tok,
+                    &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
+                    &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
+                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po})
+    b->release();
+  delete e;
+}
+
+int wm_set_weight(wm_engine* e, const char* name, const void* d_src, int64_t nbytes, void* stream) {
+  return guarded(e, [&] {
+    auto it = e->slots.find(name);
+    if (it == e->slots.end()) throw std::runtime_error(std::string("wm_set_weight: unknown weight ") + name);
+    if ((size_t)nbytes != it->second.bytes)
+      throw std::runtime_error(std::string("wm_set_weight: ") + name + " expects " + std::to_string(it->second.bytes) +
+                               " bytes, got " + std::to_string(nbytes));
+    HIP_OK(hipMemcpyAsync((char*)e->arena.p + it->second.off, d_src, nbytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    it->second.set = true;
+  });
+}
+
+int32_t wm_weights_complete(wm_engine* e) {
+  if (!e) return 0;
+  for (auto& kv : e->slots)
+    if (!kv.second.set) return 0;
+  return 1;
+}
+
+int wm_logmel(wm_engine* e, const float* d_pcm, int64_t pcm_offset, int64_t n_samples, int64_t frame0, int32_t n_frames,
+              float* d_mel, int64_t ld, uint32_t* d_gmax, void* stream) {
+  return guarded(e, [&] {
+    const long long n_padded = n_samples + 160;
+    launch_logmel(d_pcm, pcm_offset, n_samples, n_padded, frame0, n_frames, e->fe_window.as<float>(), e->fe_cos.as<float>(),
+                  e->fe_sin.as<float>(), e->fe_filt.as<float>(), e->fe_lo.as<int>(), e->fe_hi.as<int>(), e->dm.n_mels,
+                  d_mel, ld, d_gmax, (hipStream_t)stream);
+  });
+}
+
+int wm_logmel_finalize(wm_engine* e, float* d_mel, int64_t n_frames, int64_t ld, const uint32_t* d_gmax, const float* h_gmax,
+                       float* h_gmax_out, void* stream) {
+  return guarded(e, [&] {
+    hipStream_t st = (hipStream_t)stream;
+    e->s_pm.ensure(64);
+    float* gm = e->s_pm.as<float>();
+    if (h_gmax) HIP_OK(hipMemcpyAsync(gm, h_gmax, 4, hipMemcpyHostToDevice, st));
+    else launch_ordered_to_float(d_gmax, gm, st);
+    if (h_gmax_out) {
+      HIP_OK(hipMemcpyAsync(h_gmax_out, gm, 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+    }
+    launch_logmel_clamp(d_mel, e->dm.n_mels, n_frames, ld, nullptr, gm, st);
+    if (h_gmax) HIP_OK(hipStreamSynchronize(st));
+  });
+}
+
+int wm_encode(wm_engine* e, const float* d_mel, int64_t ld, const int32_t* h_seek, const int32_t* h_nframes, int32_t B,
+              void* d_enc_out, void* stream) {
+  return guarded(e, [&] {
+    check_weights(e);
+    hipStream_t st = (hipStream_t)stream;
+    const int chunk = 16;
+    const size_t per = (size_t)e->dm.n_audio_ctx * e->dm.n_state;
+    for (int b0 = 0; b0 < B; b0 += chunk) {
+      const int nb = std::min(chunk, B - b0);
+      for (int i = 0; i < nb; ++i)
+        if (h_nframes[b0 + i] < 0 || h_nframes[b0 + i] > 3000 || h_seek[b0 + i] < 0 || h_seek[b0 + i] + h_nframes[b0 + i] > ld)
+          throw std::runtime_error("wm_encode: window outside the mel buffer");
+      encode_chunk(e, d_mel, ld, h_seek + b0, h_nframes + b0, nb, (bf16*)d_enc_out + (size_t)b0 * per, st);
+      HIP_OK(hipStreamSynchronize(st));   // seek/len staging buffers are reused by the next chunk
+    }
+  });
+}
+
+int wm_reserve(wm_engine* e, int32_t n_slots, int32_t n_hyp, void* stream) {
+  return guarded(e, [&] {
+    (void)stream;
+    reserve(e, n_slots, n_hyp);
+  });
+}
+
+int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void* stream) {
+  return guarded(e, [&] {
+    check_weights(e);
+    if (slot0 < 0 || slot0 + B > e->n_slots) throw std::runtime_error("wm_cross_kv: slots out of range (wm_reserve first)");
+    const auto& m = e->dm;
+    const int d = m.n_state, T = m.n_audio_ctx;
+    GemmEpi ep = epi_of(EPI_CROSS_KV, e->ckv.p, 0, e->Wf("dec.ckv.b"));
+    ep.rpb = T; ep.d = d; ep.head_dim = 64; ep.n_head = m.n_head; ep.n_slots = e->n_slots; ep.slot0 = slot0;
+    launch_gemm(amat((const bf16*)d_enc, d), e->Wb("dec.ckv.w"), d, B * T, m.n_dec_layer * 2 * d, d, ep, (hipStream_t)stream);
+  });
+}
+
+int wm_generate(wm_engine* e, const wm_generate_args* a, void* stream) {
+  return guarded(e, [&] { generate(e, a, (hipStream_t)stream); });
+}
+
+int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_len, const int32_t* h_tokens, float* d_logits,
+               int32_t last_only, const int32_t* h_align_heads, int32_t n_align, float* d_attn, void* stream) {
+  return guarded(e, [&] {
+    forward(e, n_seq, h_slots, seq_len, h_tokens, d_logits, last_only, h_align_heads, n_align, d_attn, (hipStream_t)stream);
+  });
+}
+
+int64_t wm_device_bytes(wm_engine* e) { return e ? (int64_t)e->device_bytes() : 0; }
+
+}  // extern "C"

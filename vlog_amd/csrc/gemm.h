@@ -1,0 +1,41 @@
+// bf16 MFMA GEMM  C[M,N] = A[M,K] . W[N,K]^T  with fused epilogues (gfx950).
+#pragma once
+#include "common.h"
+
+struct GemmA {
+  const bf16* ptr;
+  long long ld;        // elements between consecutive rows
+  int rpb;             // rows per batch (0: plain 2-D)
+  long long bstride;   // elements between batches
+};
+
+// Epilogue kinds (see gemm.hip for the exact formulas)
+enum EpiKind {
+  EPI_BF16 = 0,        // C_bf16[r,c] = act(acc + bias[c]); row r -> (r/rpb)*bstride + (r%rpb + roff)*ldc
+  EPI_RESID_F32 = 1,   // X_f32[r,c] += acc + bias[c]
+  EPI_GELU_POS_F32 = 2,// X_f32[r,c]  = gelu(acc + bias[c]) + pos[r % rpb, c]
+  EPI_F32 = 3,         // C_f32[r,c]  = acc (+ bias)
+  EPI_DEC_QKV = 4,     // decoder self-attn: q -> C_bf16, k/v -> self-KV cache at (row_hyp[r], row_pos[r])
+  EPI_CROSS_KV = 5,    // cross-KV projection -> [L][2][slots][H][T][hd]
+};
+
+struct GemmEpi {
+  int kind;
+  int act;                 // EPI_BF16: 0 none, 1 gelu
+  const float* bias;       // [N] or nullptr
+  void* out;               // bf16* or float*
+  long long ldc;
+  int rpb;                 // output rows per batch (EPI_BF16, EPI_GELU_POS_F32, EPI_CROSS_KV: T)
+  long long bstride;
+  int roff;
+  const float* pos;        // EPI_GELU_POS_F32
+  // EPI_DEC_QKV
+  bf16* kcache; bf16* vcache;       // layer base of the self-KV cache, [n_hyp_max][H][n_ctx][hd]
+  const int* row_hyp; const int* row_pos;
+  int d, n_head, head_dim, n_ctx;
+  // EPI_CROSS_KV
+  int n_slots, slot0;
+};
+
+void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
+                 hipStream_t st);

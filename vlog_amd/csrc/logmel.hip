@@ -1,0 +1,131 @@
+// Log-mel frontend for gfx950: reflect-centred STFT (n_fft 400, hop 160, periodic Hann) -> |X|^2 ->
+// slaney mel filterbank -> log10(max(., 1e-10)), plus a global max for the max-8 clamp.
+//
+// Replaces faster-whisper's numpy FeatureExtractor.__call__ [FW↑] (reference call site
+// worker/transcription.py:105-111; restated in oracle/mel.py).  n_fft = 400 = 2^4 * 5^2 is not a power
+// of two, so the transform is a direct DFT from an LDS twiddle table (exact f32 fmaf chains, accurate to
+// the 1e-4 log-mel gate); the whole frontend is ~1 GFLOP per 30 s window against 2.3 TFLOP for the
+// large-v3 encoder, so its roofline is irrelevant next to the encoder.
+//
+// Frames are indexed GLOBALLY over the file so a shard (one GPU's window range) computes exactly the
+// frames the whole-file spectrogram would: global padded sample i maps to file sample s = i - 200 with
+// numpy "reflect" at the file edges over x_pad = pcm ++ zeros(pad_tail).
+#include "common.h"
+#include <stdexcept>
+#include <string>
+
+#define NFFT 400
+#define NBIN 201
+#define HOP 160
+#define FPB 8          // frames per block
+
+__global__ __launch_bounds__(256) void logmel_kernel(
+    const float* __restrict__ pcm, long long pcm_offset, long long n_samples, long long n_padded,
+    long long frame0, int n_frames, const float* __restrict__ window, const float* __restrict__ twc,
+    const float* __restrict__ tws, const float* __restrict__ filt, const int* __restrict__ flo,
+    const int* __restrict__ fhi, int n_mels, float* __restrict__ out, long long ld,
+    unsigned int* __restrict__ gmax) {
+  __shared__ float s_x[FPB][NFFT];
+  __shared__ float s_c[NFFT];
+  __shared__ float s_s[NFFT];
+  __shared__ float s_p[FPB][NBIN + 3];
+  __shared__ float s_red[4];
+  const int tid = threadIdx.x;
+  const long long fb = (long long)blockIdx.x * FPB;   // first local frame of this block
+
+  for (int i = tid; i < NFFT; i += 256) { s_c[i] = twc[i]; s_s[i] = tws[i]; }
+  for (int i = tid; i < FPB * NFFT; i += 256) {
+    const int f = i / NFFT, n = i - f * NFFT;
+    float v = 0.f;
+    const long long lf = fb + f;
+    if (lf < n_frames) {
+      long long s = (frame0 + lf) * HOP + n - NFFT / 2;      // file sample index before reflection
+      if (s < 0) s = -s;
+      if (s >= n_padded) s = 2 * (n_padded - 1) - s;
+      if (s < n_samples) v = pcm[s - pcm_offset];
+      v *= window[n];
+    }
+    s_x[f][n] = v;
+  }
+  __syncthreads();
+
+  // Direct DFT: one (frame, bin) per work item; twiddle index (k*n) mod 400 advanced incrementally.
+  for (int it = tid; it < FPB * NBIN; it += 256) {
+    const int f = it / NBIN, k = it - f * NBIN;
+    float re = 0.f, im = 0.f;
+    int idx = 0;
+    const float* x = s_x[f];
+#pragma unroll 4
+    for (int n = 0; n < NFFT; ++n) {
+      const float xv = x[n];
+      re = fmaf(xv, s_c[idx], re);
+      im = fmaf(xv, s_s[idx], im);
+      idx += k;
+      if (idx >= NFFT) idx -= NFFT;
+    }
+    s_p[f][k] = fmaf(re, re, im * im);
+  }
+  __syncthreads();
+
+  float lmax = -INFINITY;
+  for (int it = tid; it < FPB * n_mels; it += 256) {
+    const int m = it / FPB, f = it - m * FPB;
+    const long long lf = fb + f;
+    if (lf >= n_frames) continue;
+    const float* w = filt + (long long)m * NBIN;
+    float acc = 0.f;
+    for (int k = flo[m]; k < fhi[m]; ++k) acc = fmaf(w[k], s_p[f][k], acc);
+    const float lv = log10f(fmaxf(acc, 1e-10f));
+    out[(long long)m * ld + lf] = lv;
+    lmax = fmaxf(lmax, lv);
+  }
+  lmax = wave_max(lmax);
+  if ((tid & 63) == 0) s_red[tid >> 6] = lmax;
+  __syncthreads();
+  if (tid == 0) {
+    float m = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
+    if (m > -INFINITY) atomicMax(gmax, float_to_ordered(m));
+  }
+}
+
+__global__ void logmel_clamp_kernel(float* __restrict__ mel, long long rows, long long cols, long long ld,
+                                    const unsigned int* __restrict__ gmax, const float* __restrict__ gmax_f) {
+  const float g = gmax_f ? gmax_f[0] : ordered_to_float(gmax[0]);
+  const float lo = g - 8.0f;
+  const long long n = rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cols, c = i - r * cols;
+    float* p = mel + r * ld + c;
+    *p = (fmaxf(*p, lo) + 4.0f) * 0.25f;
+  }
+}
+
+__global__ void ordered_to_float_kernel(const unsigned int* __restrict__ in, float* __restrict__ out) {
+  out[0] = ordered_to_float(in[0]);
+}
+
+void launch_logmel(const float* pcm, long long pcm_offset, long long n_samples, long long n_padded,
+                   long long frame0, int n_frames, const float* window, const float* twc, const float* tws,
+                   const float* filt, const int* flo, const int* fhi, int n_mels, float* out, long long ld,
+                   unsigned int* gmax, hipStream_t st) {
+  if (n_frames <= 0) return;
+  dim3 grid((n_frames + FPB - 1) / FPB);
+  hipLaunchKernelGGL(logmel_kernel, grid, dim3(256), 0, st, pcm, pcm_offset, n_samples, n_padded, frame0,
+                     n_frames, window, twc, tws, filt, flo, fhi, n_mels, out, ld, gmax);
+  WM_LAUNCH_CHECK("logmel_kernel");
+}
+
+void launch_logmel_clamp(float* mel, long long rows, long long cols, long long ld, const unsigned int* gmax,
+                         const float* gmax_f, hipStream_t st) {
+  long long n = rows * cols;
+  if (n <= 0) return;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(logmel_clamp_kernel, dim3(blocks), dim3(256), 0, st, mel, rows, cols, ld, gmax, gmax_f);
+  WM_LAUNCH_CHECK("logmel_clamp_kernel");
+}
+
+void launch_ordered_to_float(const unsigned int* in, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(ordered_to_float_kernel, dim3(1), dim3(1), 0, st, in, out);
+  WM_LAUNCH_CHECK("ordered_to_float_kernel");
+}

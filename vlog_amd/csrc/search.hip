@@ -1,0 +1,367 @@
+// On-device decoding search for gfx950: Whisper logit rules + log-softmax + greedy / sampling / beam
+// candidate selection, and per-window beam bookkeeping.  Restates what CTranslate2's Whisper generate does
+// on the host side of each step [FW↑] (oracle: oracle/decode.py; timestamp rules pinned against
+// transformers WhisperTimeStampLogitsProcessor):
+//   1. SuppressBlank (first sampled step: " " and <|endoftext|>), 2. SuppressTokens (mask), 3. timestamp
+//   rules (no <|notimestamps|>; pairs; monotonic; first token a timestamp <= max_initial; if the timestamp
+//   log-mass beats the best text token, only timestamps remain).
+// One 1024-thread workgroup per hypothesis row streams the 51,866-wide logits row twice (max, then
+// sum-exp) per segment (text / timestamps), so the forcing rule and the final normaliser come out of two
+// segment log-sum-exps without a third pass.  Greedy and sampling (Gumbel-max over logits / T) update the
+// sequence state in the same kernel; beam search emits each hypothesis's top beam+1 candidates and a
+// per-window kernel ranks them (openai BeamSearchDecoder semantics, patience, finished list).
+#include "search.h"
+#include <stdexcept>
+#include <string>
+
+#define SB 1024
+#define NW (SB / 64)
+#define KMAX 9
+
+struct Cand { float v; int i; };
+__device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) { return v1 > v2 || (v1 == v2 && i1 < i2); }
+
+__device__ __forceinline__ void topk_insert(Cand (&L)[KMAX], int K, float x, int i) {
+  if (!better(x, i, L[K - 1].v, L[K - 1].i)) return;
+  Cand c{x, i};
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j)
+    if (j < K && better(c.v, c.i, L[j].v, L[j].i)) { Cand t = L[j]; L[j] = c; c = t; }
+}
+
+// Wave-level extraction of the K best from every lane's sorted list; lane 0 writes them to dst[0..K).
+__device__ __forceinline__ void wave_topk(Cand (&L)[KMAX], int K, Cand* dst) {
+  const int lane = threadIdx.x & 63;
+  for (int r = 0; r < K; ++r) {
+    Cand best = L[0];
+    int owner = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(best.v, o, 64);
+      const int i2 = __shfl_xor(best.i, o, 64);
+      const int ow2 = __shfl_xor(owner, o, 64);
+      if (better(v2, i2, best.v, best.i) || (v2 == best.v && i2 == best.i && ow2 < owner)) {
+        best.v = v2; best.i = i2; owner = ow2;
+      }
+    }
+    if (lane == 0) dst[r] = best;
+    if (lane == owner) {
+#pragma unroll
+      for (int j = 0; j < KMAX - 1; ++j) L[j] = L[j + 1];
+      L[KMAX - 1] = Cand{-INFINITY, 0x7fffffff};
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ float gumbel(unsigned long long seed, int hyp, int step, int i) {
+  unsigned long long h = mix64(seed ^ mix64(((unsigned long long)hyp << 40) ^ ((unsigned long long)step << 20) ^ (unsigned long long)i));
+  const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
+  return -logf(-logf(u));
+}
+
+// block-wide (max, argmax) reduce; returns result in all threads
+__device__ Cand block_argmax(Cand c, Cand* sh) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(c.v, o, 64);
+    const int i2 = __shfl_xor(c.i, o, 64);
+    if (better(v2, i2, c.v, c.i)) { c.v = v2; c.i = i2; }
+  }
+  __syncthreads();
+  if (lane == 0) sh[wv] = c;
+  __syncthreads();
+  Cand r = sh[0];
+  for (int w = 1; w < NW; ++w)
+    if (better(sh[w].v, sh[w].i, r.v, r.i)) r = sh[w];
+  return r;
+}
+__device__ float block_sum(float v, float* sh) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[wv] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int w = 0; w < NW; ++w) r += sh[w];
+  return r;
+}
+
+__global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
+  __shared__ Cand sh_c[NW];
+  __shared__ float sh_f[NW];
+  __shared__ int s_info[4];
+  __shared__ Cand s_top[2][NW * KMAX];
+  const int h = blockIdx.x, tid = threadIdx.x;
+  if (p.done[h]) return;
+  const int len = p.seq_len[h];
+  const int* seq = p.tokens + (long long)h * p.n_ctx;
+  const int tb = p.ts_begin;
+  if (tid == 0) {
+    const int ns = len - p.sample_begin;
+    const int last = ns >= 1 ? seq[len - 1] : -1;
+    const int last_ts = ns >= 1 && last >= tb;
+    const int pen_ts = ns < 2 || seq[len - 2] >= tb;
+    int lastv = -1;
+    for (int i = len - 1; i >= p.sample_begin; --i)
+      if (seq[i] >= tb) { lastv = seq[i]; break; }
+    int bound = tb;                          // timestamps in [tb, bound) are masked
+    if (lastv >= 0) bound = (last_ts && !pen_ts) ? lastv : lastv + 1;
+    s_info[0] = ns == 0;
+    s_info[1] = (last_ts && pen_ts) ? 1 : ((last_ts && !pen_ts) ? 2 : 0);
+    s_info[2] = bound;
+  }
+  __syncthreads();
+  const int first = s_info[0], pair_rule = s_info[1], bound = s_info[2];
+  const float* lg = p.logits + (long long)h * p.ldl;
+  const int V = p.V;
+  const bool ts_on = p.with_ts != 0;
+  auto masked = [&](int i) -> bool {
+    if (p.suppress[i]) return true;
+    if (first && p.suppress_blank && (i == p.blank || i == p.eot)) return true;
+    if (!ts_on) return false;
+    if (i == p.no_timestamps) return true;
+    if (i >= tb) {
+      if (pair_rule == 1) return true;
+      if (i < bound) return true;
+      if (first && p.max_initial >= 0 && i > tb + p.max_initial) return true;
+    } else {
+      if (pair_rule == 2 && i < p.eot) return true;
+      if (first) return true;
+    }
+    return false;
+  };
+  // pass 1: per-segment max / argmax (and Gumbel keys for sampling, local top-k for beam)
+  Cand mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
+  Cand gt{-INFINITY, 0x7fffffff}, gs{-INFINITY, 0x7fffffff};
+  Cand kt[KMAX], ks[KMAX];
+  const int K = p.mode == 1 ? p.topk : 0;
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) { kt[j] = Cand{-INFINITY, 0x7fffffff}; ks[j] = kt[j]; }
+  for (int i = tid; i < V; i += SB) {
+    if (masked(i)) continue;
+    const float x = lg[i];
+    const bool is_ts = i >= tb;
+    Cand& m = is_ts ? ms : mt;
+    if (better(x, i, m.v, m.i)) { m.v = x; m.i = i; }
+    if (p.mode == 2) {
+      const float key = x * p.inv_temperature + gumbel(p.seed, h, p.step, i);
+      Cand& gg = is_ts ? gs : gt;
+      if (better(key, i, gg.v, gg.i)) { gg.v = key; gg.i = i; }
+    } else if (K) {
+      if (is_ts) topk_insert(ks, K, x, i);
+      else topk_insert(kt, K, x, i);
+    }
+  }
+  mt = block_argmax(mt, sh_c);
+  ms = block_argmax(ms, sh_c);
+  // pass 2: sum-exp per segment
+  float st = 0.f, ss = 0.f;
+  for (int i = tid; i < V; i += SB) {
+    if (masked(i)) continue;
+    const float x = lg[i];
+    if (i >= tb) ss += expf(x - ms.v);
+    else st += expf(x - mt.v);
+  }
+  st = block_sum(st, sh_f);
+  ss = block_sum(ss, sh_f);
+  const float lse_t = mt.v > -INFINITY ? mt.v + logf(st) : -INFINITY;
+  const float lse_s = ms.v > -INFINITY ? ms.v + logf(ss) : -INFINITY;
+  const bool forced = ts_on && lse_s > mt.v;
+  float Z;
+  if (forced) Z = lse_s;
+  else if (lse_t == -INFINITY) Z = lse_s;
+  else if (lse_s == -INFINITY) Z = lse_t;
+  else Z = fmaxf(lse_t, lse_s) + log1pf(expf(-fabsf(lse_t - lse_s)));
+
+  if (p.mode == 1) {
+    // merge local top-k lists: wave-level extraction, then thread 0 merges the per-wave winners
+    const int wv = tid >> 6;
+    wave_topk(kt, K, &s_top[0][wv * KMAX]);
+    wave_topk(ks, K, &s_top[1][wv * KMAX]);
+    __syncthreads();
+    if (tid == 0) {
+      int out = 0;
+      int ptr_t[NW], ptr_s[NW];
+      for (int w = 0; w < NW; ++w) { ptr_t[w] = 0; ptr_s[w] = 0; }
+      for (int r = 0; r < K; ++r) {
+        Cand best{-INFINITY, 0x7fffffff};
+        int bw = -1, bseg = 0;
+        for (int seg = forced ? 1 : 0; seg < 2; ++seg)
+          for (int w = 0; w < NW; ++w) {
+            const int pp = seg ? ptr_s[w] : ptr_t[w];
+            if (pp >= K) continue;
+            const Cand c = s_top[seg][w * KMAX + pp];
+            if (better(c.v, c.i, best.v, best.i)) { best = c; bw = w; bseg = seg; }
+          }
+        if (bw < 0 || best.v == -INFINITY) {
+          p.cand_tok[(long long)h * p.topk + out] = -1;
+          p.cand_lp[(long long)h * p.topk + out] = -INFINITY;
+        } else {
+          if (bseg) ++ptr_s[bw]; else ++ptr_t[bw];
+          p.cand_tok[(long long)h * p.topk + out] = best.i;
+          p.cand_lp[(long long)h * p.topk + out] = best.v - Z;
+        }
+        ++out;
+      }
+    }
+    return;
+  }
+
+  if (p.mode == 2) {
+    gt = block_argmax(gt, sh_c);
+    gs = block_argmax(gs, sh_c);
+  }
+  if (tid == 0) {
+    int tok;
+    if (p.mode == 2) tok = forced ? gs.i : (better(gt.v, gt.i, gs.v, gs.i) ? gt.i : gs.i);
+    else tok = forced ? ms.i : (better(mt.v, mt.i, ms.v, ms.i) ? mt.i : ms.i);
+    const float lp = lg[tok] - Z;
+    p.cum[h] += lp;
+    bool fin = false;
+    if (tok == p.eot) {
+      fin = true;
+    } else {
+      p.tokens[(long long)h * p.n_ctx + len] = tok;
+      p.seq_len[h] = len + 1;
+      p.row_tok[h] = tok;
+      p.row_pos[h] = len;
+      if (len + 1 >= p.max_length) fin = true;
+    }
+    if (fin) {
+      p.done[h] = 1;
+      atomicSub(p.n_active, 1);
+    }
+  }
+}
+
+void launch_logits_select(const SearchParams& p, int n_hyp, hipStream_t st) {
+  if (n_hyp <= 0) return;
+  if (p.mode == 1 && (p.topk < 1 || p.topk > KMAX)) throw std::runtime_error("beam size must be <= 8");
+  hipLaunchKernelGGL(logits_select_kernel, dim3(n_hyp), dim3(SB), 0, st, p);
+  WM_LAUNCH_CHECK("logits_select_kernel");
+}
+
+// ------------------------------------------------------------------------------------ beam bookkeeping
+#define BMAX 8
+#define CMAX 16
+
+__global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
+  __shared__ int s_tok[BMAX][448];
+  __shared__ int s_lin[BMAX][448];
+  __shared__ int s_par[BMAX], s_new[BMAX];
+  __shared__ float s_sc[BMAX];
+  __shared__ int s_nlive, s_len;
+  const int w = blockIdx.x, tid = threadIdx.x;
+  const int K = p.beam, h0 = w * K;
+  if (p.done[h0]) return;
+  const int len = p.seq_len[h0];
+  for (int i = tid; i < K * len; i += blockDim.x) {
+    const int b = i / len, t = i - b * len;
+    s_tok[b][t] = p.tokens[(long long)(h0 + b) * p.n_ctx + t];
+    s_lin[b][t] = p.lin[(long long)(h0 + b) * p.n_ctx + t];
+  }
+  if (tid == 0) {
+    // candidates in (beam, rank) order, then a stable sort by score
+    float sc[BMAX * (BMAX + 1)];
+    int src[BMAX * (BMAX + 1)], tk[BMAX * (BMAX + 1)];
+    int n = 0;
+    const int T = K + 1;
+    for (int j = 0; j < K; ++j) {
+      const float c = p.cum[h0 + j];
+      if (c == -INFINITY) continue;
+      for (int r = 0; r < T; ++r) {
+        const int t = p.cand_tok[(long long)(h0 + j) * T + r];
+        if (t < 0) continue;
+        sc[n] = c + p.cand_lp[(long long)(h0 + j) * T + r]; src[n] = j; tk[n] = t; ++n;
+      }
+    }
+    for (int a = 1; a < n; ++a) {              // insertion sort, stable, descending
+      const float v = sc[a]; const int s = src[a], t = tk[a];
+      int b = a - 1;
+      while (b >= 0 && sc[b] < v) { sc[b + 1] = sc[b]; src[b + 1] = src[b]; tk[b + 1] = tk[b]; --b; }
+      sc[b + 1] = v; src[b + 1] = s; tk[b + 1] = t;
+    }
+    int nlive = 0;
+    int nf = p.n_fin[w];
+    for (int c = 0; c < n && nlive < K; ++c) {
+      if (tk[c] == p.eot) {
+        if (nf < p.max_cand) {
+          const int b = src[c];
+          int* dst = p.fin_tok + ((long long)w * p.max_cand + nf) * p.n_ctx;
+          for (int t = p.sample_begin; t < len; ++t) dst[t - p.sample_begin] = s_tok[b][t];
+          p.fin_len[w * p.max_cand + nf] = len - p.sample_begin;
+          p.fin_cum[w * p.max_cand + nf] = sc[c];
+          ++nf;
+        }
+      } else {
+        s_par[nlive] = src[c]; s_new[nlive] = tk[c]; s_sc[nlive] = sc[c]; ++nlive;
+      }
+    }
+    p.n_fin[w] = nf;
+    s_nlive = nlive;
+    s_len = len;
+    const bool fin = nf >= p.max_cand || len + 1 >= p.max_length || nlive == 0;
+    if (fin) {
+      for (int j = 0; j < K; ++j) p.done[h0 + j] = 1;
+      atomicSub(p.n_active, K);
+    }
+  }
+  __syncthreads();
+  const int nlive = s_nlive;
+  // write the new beams (beams beyond nlive are marked dead with cum = -inf)
+  for (int i = tid; i < K * len; i += blockDim.x) {
+    const int b = i / len, t = i - b * len;
+    const int par = b < nlive ? s_par[b] : s_par[0];
+    p.tokens[(long long)(h0 + b) * p.n_ctx + t] = s_tok[par][t];
+    p.lin[(long long)(h0 + b) * p.n_ctx + t] = s_lin[par][t];
+  }
+  __syncthreads();
+  if (tid < K) {
+    const int b = tid;
+    const int par = b < nlive ? s_par[b] : s_par[0];
+    const int tok = b < nlive ? s_new[b] : s_new[0];
+    p.tokens[(long long)(h0 + b) * p.n_ctx + len] = tok;
+    p.lin[(long long)(h0 + b) * p.n_ctx + len] = h0 + b;      // the next step writes KV at (hyp, len)
+    p.seq_len[h0 + b] = len + 1;
+    p.cum[h0 + b] = b < nlive ? s_sc[b] : -INFINITY;
+    p.row_tok[h0 + b] = tok;
+    p.row_pos[h0 + b] = len;
+    (void)par;
+  }
+}
+
+void launch_beam_select(const BeamParams& p, int n_win, hipStream_t st) {
+  if (n_win <= 0) return;
+  if (p.beam > BMAX || p.max_cand > CMAX || p.n_ctx > 448) throw std::runtime_error("beam_select: limits exceeded");
+  hipLaunchKernelGGL(beam_select_kernel, dim3(n_win), dim3(256), 0, st, p);
+  WM_LAUNCH_CHECK("beam_select_kernel");
+}
+
+// softmax(logits[r])[no_speech]
+__global__ __launch_bounds__(SB) void no_speech_kernel(const float* __restrict__ logits, long long ldl, int V, int ns,
+                                                        float* __restrict__ out) {
+  __shared__ Cand sh_c[NW];
+  __shared__ float sh_f[NW];
+  const float* lg = logits + (long long)blockIdx.x * ldl;
+  Cand m{-INFINITY, 0};
+  for (int i = threadIdx.x; i < V; i += SB)
+    if (lg[i] > m.v) { m.v = lg[i]; m.i = i; }
+  m = block_argmax(m, sh_c);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < V; i += SB) s += expf(lg[i] - m.v);
+  s = block_sum(s, sh_f);
+  if (threadIdx.x == 0) out[blockIdx.x] = expf(lg[ns] - m.v) / s;
+}
+
+void launch_no_speech(const float* logits, long long ldl, int V, int rows, int no_speech, float* out, hipStream_t st) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(no_speech_kernel, dim3(rows), dim3(SB), 0, st, logits, ldl, V, no_speech, out);
+  WM_LAUNCH_CHECK("no_speech_kernel");
+}
