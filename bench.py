@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: Whisper transcription RTFx (audio-seconds per wall-second) on MI355X.
+
+Workload (BASELINE.json config 4, per GPU): large-v3, bf16, greedy with timestamps, 150 x 30 s windows of the
+seeded speech-like corpus per GPU (window-sharded: GPU r owns windows [150 r, 150 r + 150) of one long file;
+weak scaling).  One "step" = the whole hot path over the GPU's 150 windows with the PCM already resident in
+HBM: log-mel of the shard (+ the one-float global-max exchange between shards, the path's only cross-shard
+value) -> clamp -> encoder -> cross-KV -> batched greedy decode with on-device timestamp rules -> host
+segment split + detokenise + WebVTT string.  Weights are seeded random-init large-v3 weights (no checkpoints
+offline) with the <|endoftext|> direction planted so windows end after a speech-like token count
+(vlog_amd/weights.py plant_eot); the JSON reports the actual tokens per window.
+
+Prints ONE JSON line on rank 0.  `python bench.py` (N=1) or torch.distributed.run --nproc-per-node N.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from vlog_amd.audio import speech_like  # noqa: E402
+from vlog_amd.dims import model_dims  # noqa: E402
+from vlog_amd.segments import split_segments_by_timestamps  # noqa: E402
+from vlog_amd.tokenizer import Tokenizer  # noqa: E402
+from vlog_amd.vtt import generate_webvtt  # noqa: E402
+from vlog_amd.weights import synthetic_state_dict  # noqa: E402
+
+METRIC = "audio-sec transcribed per wall-sec (RTFx), large-v3, 1/2/4/8 MI355X; WER delta"
+HBM_PEAK_GBS = 8000.0
+MFMA_BF16_PEAK_TFS = 2500.0
+CLIP = 480000
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_shard(rank: int, W: int):
+    """PCM of windows [rank*W, rank*W+W) plus 200-sample margins from the neighbouring clips."""
+    g0 = rank * W
+    clips = [speech_like(30.0, g0 + i) for i in range(W)]
+    left = speech_like(30.0, g0 - 1)[-200:] if g0 > 0 else np.zeros(0, np.float32)
+    right = speech_like(30.0, g0 + W)[:200]
+    return np.concatenate([left] + clips + [right]).astype(np.float32), len(left)
+
+
+class Pipeline:
+    def __init__(self, eng, tok, dims, rank, world, W, beam, pcm_dev, margin_left, n_total):
+        self.eng, self.tok, self.dims = eng, tok, dims
+        self.rank, self.world, self.W, self.beam = rank, world, W, beam
+        self.pcm_dev, self.margin_left, self.n_total = pcm_dev, margin_left, n_total
+        st = dims.specials
+        self.prompt = [st.sot, st.lang_token("en"), st.transcribe]
+        self.suppress = list(tok.suppressed_tokens([-1]))
+        self.stage = {}
+
+    def step(self):
+        eng, W, d = self.eng, self.W, self.dims
+        t0 = time.perf_counter()
+        frame0 = self.rank * W * 3000
+        mel, gmax = eng.logmel(self.pcm_dev, n_samples=self.n_total, pcm_offset=frame0 * 160 - self.margin_left,
+                               frame0=frame0, n_frames=W * 3000)
+        g = torch.tensor([eng.gmax_value(gmax)], dtype=torch.float32)
+        if self.world > 1:
+            import torch.distributed as dist
+            gd = g.to(eng.device)
+            dist.all_reduce(gd, op=dist.ReduceOp.MAX)
+            g = gd.cpu()
+        eng.logmel_finalize(mel, gmax, float(g[0]))
+        t1 = time.perf_counter()
+        enc = eng.encode(mel, [i * 3000 for i in range(W)], [3000] * W)
+        eng.cross_kv(enc, 0)
+        torch.cuda.synchronize(eng.device)
+        t2 = time.perf_counter()
+        res, steps = eng.generate(list(range(W)), [self.prompt] * W, beam_size=self.beam, suppress_tokens=self.suppress,
+                                  max_length=448, check_every=8)
+        t3 = time.perf_counter()
+        segs = []
+        for w, r in enumerate(res):
+            off = (self.rank * W + w) * 30.0
+            cur, _, _ = split_segments_by_timestamps(r.tokens, d.specials.timestamp_begin, off, 3000, 30.0, w * 3000)
+            for s in cur:
+                text = self.tok.decode(s["tokens"])
+                if s["start"] == s["end"] or not text.strip():
+                    continue
+                segs.append({"start": s["start"], "end": s["end"], "text": text})
+        vtt = generate_webvtt(segs)
+        t4 = time.perf_counter()
+        for k, v in (("logmel", t1 - t0), ("encode", t2 - t1), ("decode", t3 - t2), ("host", t4 - t3)):
+            self.stage[k] = self.stage.get(k, 0.0) + v
+        self.last = dict(tokens=[len(r.tokens) for r in res], steps=steps, segments=len(segs), vtt_bytes=len(vtt))
+        del enc, mel
+
+
+def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
+    """Oracle (numpy fp32, this repo's CPU restatement) on the host cores: one 30 s window's log-mel + encoder,
+    plus `decode_steps` greedy decoder steps, extrapolated to the GPU run's mean tokens per window."""
+    sys.path.insert(0, ROOT)
+    from oracle import mel as omel
+    from oracle.decode import GenerateOptions, generate_one
+    from oracle.model import OracleWhisper
+    from vlog_amd.weights import round_bf16
+
+    st = dims.specials
+    orc = OracleWhisper(round_bf16(sd), dims, np.float32)
+    x = speech_like(30.0, 0)
+    t0 = time.perf_counter()
+    f = omel.log_mel(x, dims.n_mels)
+    enc = orc.encode(omel.pad_or_trim(f)[None])
+    cross = orc.cross_kv(enc)
+    t1 = time.perf_counter()
+    prompt = [st.sot, st.lang_token("en"), st.transcribe]
+    r = generate_one(orc, cross, prompt, st, GenerateOptions(max_length=len(prompt) + decode_steps))
+    t2 = time.perf_counter()
+    n_steps = max(1, len(r.tokens))
+    per_step = (t2 - t1) / n_steps
+    per_window = (t1 - t0) + per_step * max(mean_tokens, 1.0)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": round(30.0 / per_window, 4), "unit": "audio_s/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle/ numpy fp32 CPU restatement, {dims.name}: one 30 s window log-mel+encoder+cross-KV "
+                       f"({t1 - t0:.1f} s) + {n_steps} greedy decoder steps ({per_step:.3f} s/step), extrapolated to "
+                       f"{mean_tokens:.1f} tokens/window; faster-whisper CPU baseline unavailable (not installed)")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="large-v3")
+    ap.add_argument("--windows", type=int, default=150, help="30 s windows per GPU")
+    ap.add_argument("--beam", type=int, default=1)
+    ap.add_argument("--eot-after", type=int, default=110)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--no-profile", action="store_true", help="skip the live per-kernel event timing")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    dims = model_dims(args.model)
+    t = time.perf_counter()
+    sd = synthetic_state_dict(dims, seed=0, eot_after=args.eot_after)
+    from vlog_amd.engine import GpuEngine
+    eng = GpuEngine(dims, sd, local)
+    if not (rank == 0 and world == 1 and not args.no_cpu_baseline):
+        del sd
+        sd = None
+    tok = Tokenizer(dims, language="en")
+    W = args.windows
+    pcm, margin = build_shard(rank, W)
+    pcm_dev = torch.from_numpy(pcm).to(eng.device)
+    n_total = world * W * CLIP
+    eng.reserve(W, W * max(1, args.beam))
+    log(f"[rank {rank}] setup {time.perf_counter() - t:.1f} s, engine {eng.device_bytes() / 2**30:.1f} GiB")
+    pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total)
+
+    def barrier():
+        torch.cuda.synchronize(eng.device)
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        pipe.step()
+    pipe.stage = {}
+    barrier()
+    if not args.no_profile:
+        eng.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = None
+    if not args.no_profile:
+        eng.profile(False)
+        prof = eng.profile_read()
+    if world > 1:
+        import torch.distributed as dist
+        te = torch.tensor([elapsed], device=eng.device, dtype=torch.float64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te.item())
+    audio_s = world * W * 30.0 * args.steps
+    value = audio_s / elapsed
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    toks = pipe.last["tokens"]
+    mean_tok = float(np.mean(toks))
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": f"{args.model} bf16 {'greedy' if args.beam == 1 else 'beam%d' % args.beam}, timestamps on, "
+                               f"{W} x 30 s windows per GPU of the seeded speech-like corpus, window-sharded (config 4)",
+                   "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
+                   "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
+                   "parallelism": f"window-shard x{world}", "weights": f"synthetic seed 0, eot_after={args.eot_after}"},
+        "stages_s_per_step": {k: round(v / args.steps, 4) for k, v in pipe.stage.items()},
+    }
+    if prof:
+        kern = {}
+        for k, v in prof.items():
+            if v["launches"] == 0:
+                continue
+            kern[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
+                       "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["flops"] else None,
+                       "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["bytes"] else None}
+        out["kernels"] = kern
+        dom = max(kern, key=lambda k: kern[k]["ms"])
+        v = prof[dom]
+        if dom in ("cross_attn", "self_attn", "select", "dec_other", "logmel") or (v["flops"] == 0):
+            ach = v["bytes"] / (v["ms"] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4)}
+        else:
+            ach = v["flops"] / (v["ms"] * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(ach / MFMA_BF16_PEAK_TFS, 4)}
+        roof["kernel"] = dom
+        roof["traffic"] = None
+        if os.path.isfile(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                roof["traffic"] = tj.get(dom)
+            except Exception:
+                pass
+        enc_ms = sum(prof[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
+        enc_fl = sum(prof[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
+        out["roofline"] = roof
+        out["encoder_mfma"] = {"achieved_tflops": round(enc_fl / max(enc_ms, 1e-9) / 1e9, 1),
+                               "frac_of_2500": round(enc_fl / max(enc_ms, 1e-9) / 1e9 / MFMA_BF16_PEAK_TFS, 4)}
+        cx = prof["cross_attn"]
+        out["decoder_kv_read"] = {"achieved_gbs": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6, 1),
+                                  "frac_of_8000": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6 / HBM_PEAK_GBS, 4)}
+    if world == 1 and not args.no_cpu_baseline and sd is not None:
+        try:
+            out["cpu_baseline"] = cpu_baseline(dims, sd, mean_tok)
+        except Exception as e:  # reported, never fatal to the GPU measurement
+            out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

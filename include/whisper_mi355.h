@@ -110,6 +110,16 @@ int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_
 /* Bytes of device memory held by the engine (weights + caches + scratch). */
 int64_t wm_device_bytes(wm_engine* e);
 
+/* Built-in kernel profiler (used by bench.py for the live roofline numbers): when enabled, every launch
+ * of a kernel class is bracketed by HIP events on its own stream, and the class accumulates its
+ * algorithmic FLOPs and bytes (the decoder attention kernels count the K/V bytes they actually read).
+ * wm_profile(e, 1) resets and enables, wm_profile(e, 0) disables; wm_profile_read returns launches,
+ * summed event time, FLOPs and bytes of one class. */
+int32_t wm_profile_classes(void);
+const char* wm_profile_name(int32_t cls);
+int wm_profile(wm_engine* e, int32_t enable);
+int wm_profile_read(wm_engine* e, int32_t cls, int64_t* launches, double* ms, double* flops, double* bytes);
+
 #ifdef __cplusplus
 }
 #endif

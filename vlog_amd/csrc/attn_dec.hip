@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void self_attn_kernel(const bf16* __restrict__
                                                         const int* __restrict__ lin, const int* __restrict__ row_hyp,
                                                         const int* __restrict__ row_pos, const int* __restrict__ done,
                                                         bf16* __restrict__ out, long long ldo, int rows, int H,
-                                                        int n_ctx, float scale_log2) {
+                                                        int n_ctx, float scale_log2, unsigned long long* stat) {
   __shared__ float s_sc[4][MAX_CTX];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int idx = blockIdx.x * 4 + wv;
@@ -40,6 +40,7 @@ __global__ __launch_bounds__(256) void self_attn_kernel(const bf16* __restrict__
   const int pos = row_pos[row];
   const int nk = pos + 1;
   const int sub = lane & 7, g = lane >> 3;
+  if (stat && lane == 0) atomicAdd(stat, (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
   float qf[8];
   load8(q + (long long)row * ldq + h * HD + sub * 8, qf);
 #pragma unroll
@@ -100,13 +101,13 @@ __global__ __launch_bounds__(256) void self_attn_kernel(const bf16* __restrict__
 
 void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* vc, const int* lin, const int* row_hyp,
                       const int* row_pos, const int* done, bf16* out, long long ldo, int rows, int H, int n_ctx,
-                      hipStream_t st) {
+                      unsigned long long* stat, hipStream_t st) {
   if (rows <= 0) return;
   if (n_ctx > MAX_CTX) throw std::runtime_error("self_attn: n_ctx > 448");
   const float scale_log2 = 0.125f * 1.4426950408889634f;
   dim3 grid((rows * H + 3) / 4);
   hipLaunchKernelGGL(self_attn_kernel, grid, dim3(256), 0, st, q, ldq, kc, vc, lin, row_hyp, row_pos, done, out, ldo,
-                     rows, H, n_ctx, scale_log2);
+                     rows, H, n_ctx, scale_log2, stat);
   WM_LAUNCH_CHECK("self_attn_kernel");
 }
 
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(
     long long panel, const int* __restrict__ hyp_slot, const int* __restrict__ row_hyp, const int* __restrict__ done,
     bf16* __restrict__ out, long long ldo, int H, int T, int splits, float* __restrict__ part_m,
     float* __restrict__ part_l, float* __restrict__ part_o, float* __restrict__ probs, const int* __restrict__ head_map,
-    int n_align, float scale_log2) {
+    int n_align, float scale_log2, unsigned long long* stat) {
   __shared__ float s_sc[CT_MAX];
   __shared__ float s_red[4];
   __shared__ float s_acc[4][HD];
@@ -131,6 +132,7 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(
   const int slot = hyp_slot[hyp];
   const int chunk = (T + splits - 1) / splits;
   const int k0 = split * chunk, k1 = min(T, k0 + chunk), nk = k1 - k0;
+  if (stat && tid == 0) atomicAdd(stat, (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
   const long long off = ((long long)slot * H + h) * panel;       // panel = T * HD
   const bf16* K = kbase + off;
   const bf16* V = vbase + off;
@@ -235,7 +237,7 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
 void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf16* vbase, int T, const int* hyp_slot,
                        const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H, int splits,
                        float* part_m, float* part_l, float* part_o, float* probs, const int* head_map, int n_align,
-                       hipStream_t st) {
+                       unsigned long long* stat, hipStream_t st) {
   if (rows <= 0) return;
   if (T > CT_MAX * splits) throw std::runtime_error("cross_attn: too many keys per split");
   if (probs && splits != 1) throw std::runtime_error("cross_attn: attention capture needs splits == 1");
@@ -243,7 +245,7 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
   dim3 grid(rows * H, splits);
   hipLaunchKernelGGL(cross_attn_kernel, grid, dim3(256), 0, st, q, ldq, kbase, vbase, (long long)T * HD, hyp_slot,
                      row_hyp, done, out, ldo, H, T, splits, part_m, part_l, part_o, probs, head_map, n_align,
-                     scale_log2);
+                     scale_log2, stat);
   WM_LAUNCH_CHECK("cross_attn_kernel");
   if (splits > 1) {
     hipLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, part_m, part_l, part_o, row_hyp, done,

@@ -33,9 +33,18 @@ void launch_im2col_conv1(const float*, long long, const int*, const int*, int, i
 void launch_zero_pad_rows(bf16*, int, long long, int, hipStream_t);
 void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
 void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const int*, const int*, const int*, const int*,
-                      bf16*, long long, int, int, int, hipStream_t);
+                      bf16*, long long, int, int, int, unsigned long long*, hipStream_t);
 void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
-                       long long, int, int, int, float*, float*, float*, float*, const int*, int, hipStream_t);
+                       long long, int, int, int, float*, float*, float*, float*, const int*, int, unsigned long long*,
+                       hipStream_t);
+
+// Kernel classes timed by the built-in profiler (wm_profile / wm_profile_read).
+enum ProfClass {
+  P_LOGMEL = 0, P_ENC_GEMM, P_ENC_ATTN, P_ENC_OTHER, P_CROSSKV_GEMM, P_DEC_GEMM, P_SELF_ATTN, P_CROSS_ATTN,
+  P_LOGITS_GEMM, P_SELECT, P_DEC_OTHER, P_N
+};
+static const char* kProfNames[P_N] = {"logmel", "enc_gemm", "enc_attn", "enc_other", "crosskv_gemm", "dec_gemm",
+                                      "self_attn", "cross_attn", "logits_gemm", "select", "dec_other"};
 
 namespace {
 
@@ -96,6 +105,24 @@ struct wm_engine {
   DevBuf d_prow_tok, d_prow_pos, d_prow_hyp, d_head_map;
   // step activations
   DevBuf s_x, s_hb, s_q, s_ao, s_ff, s_logits, s_pm, s_pl, s_po;
+  // profiler: per class, HIP event pairs recorded on the launch stream + algorithmic flops / bytes
+  bool prof_on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[P_N];
+  std::vector<hipEvent_t> ev_pool;
+  double prof_flops[P_N] = {0}, prof_bytes[P_N] = {0};
+  DevBuf gemm_ws;            // split-K partial slabs
+  DevBuf prof_dbytes;        // device counters (attention kernels add the bytes they actually read)
+  hipEvent_t ev_get() {
+    if (ev_pool.empty()) {
+      hipEvent_t ev;
+      HIP_OK(hipEventCreate(&ev));
+      return ev;
+    }
+    hipEvent_t ev = ev_pool.back();
+    ev_pool.pop_back();
+    return ev;
+  }
+  unsigned long long* dstat(int cls) { return prof_on ? prof_dbytes.as<unsigned long long>() + cls : nullptr; }
 
   const Slot& slot(const std::string& n) const {
     auto it = slots.find(n);
@@ -216,6 +243,39 @@ GemmEpi epi_of(int kind, void* out, long long ldc, const float* bias) {
 }
 GemmA amat(const bf16* ptr, long long ld) { return GemmA{ptr, ld, 0, 0}; }
 
+struct ProfScope {
+  wm_engine* e;
+  int cls;
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  ProfScope(wm_engine* e_, int cls_, hipStream_t st_, double flops = 0, double bytes = 0) : e(e_), cls(cls_), st(st_) {
+    if (!e->prof_on) return;
+    a = e->ev_get();
+    HIP_OK(hipEventRecord(a, st));
+    e->prof_flops[cls] += flops;
+    e->prof_bytes[cls] += bytes;
+  }
+  ~ProfScope() {
+    if (!a) return;
+    hipEvent_t b = e->ev_get();
+    (void)hipEventRecord(b, st);
+    e->prof_ev[cls].push_back({a, b});
+  }
+};
+
+// algorithmic bytes of a GEMM: A (M x K bf16) + W (N x K bf16) + output
+double gemm_bytes(double M, double N, double K, double out_bytes) { return 2 * M * K + 2 * N * K + out_bytes * M * N; }
+
+void gemm_p(wm_engine* e, int cls, const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& ep,
+            hipStream_t st) {
+  const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_F32 || ep.kind == EPI_GELU_POS_F32) ? 4 : 2;
+  ProfScope ps(e, cls, st, 2.0 * M * N * K, gemm_bytes(M, N, K, ob));
+  // split-K only where the grid is too small to fill the chip (decoder rows); 64 MB slab scratch
+  const size_t wsb = 64ull << 20;
+  e->gemm_ws.ensure(wsb);
+  launch_gemm(a, w, ldw, M, N, K, ep, e->gemm_ws.as<float>(), wsb, st);
+}
+
 // ------------------------------------------------------------------------------------------ encoder
 void encode_chunk(wm_engine* e, const float* mel, long long ld, const int* h_seek, const int* h_len, int B, bf16* out,
                   hipStream_t st) {
@@ -244,12 +304,15 @@ void encode_chunk(wm_engine* e, const float* mel, long long ld, const int* h_see
   bf16* ao = e->e_ao.as<bf16>();
   bf16* ff = e->e_ff.as<bf16>();
   // conv1 (implicit GEMM over the window-sliced mel) + GELU -> h1 rows 1..3000 of each [3001][d] block
-  launch_im2col_conv1(mel, ld, e->e_seek.as<int>(), e->e_len.as<int>(), B, m.n_mels, e->k1p, cols, st);
-  launch_zero_pad_rows(h1, B, 3001LL * d, d, st);
+  {
+    ProfScope ps(e, P_ENC_OTHER, st);
+    launch_im2col_conv1(mel, ld, e->e_seek.as<int>(), e->e_len.as<int>(), B, m.n_mels, e->k1p, cols, st);
+    launch_zero_pad_rows(h1, B, 3001LL * d, d, st);
+  }
   {
     GemmEpi ep = epi_of(EPI_BF16, h1, d, e->Wf("enc.conv1.b"));
     ep.act = 1; ep.rpb = 3000; ep.bstride = 3001LL * d; ep.roff = 1;
-    launch_gemm(amat(cols, e->k1p), e->Wb("enc.conv1.w"), e->k1p, B * 3000, d, e->k1p, ep, st);
+    gemm_p(e, P_ENC_GEMM, amat(cols, e->k1p), e->Wb("enc.conv1.w"), e->k1p, B * 3000, d, e->k1p, ep, st);
   }
   // conv2 (k3, s2): row t of window b reads h1 rows 2t-1, 2t, 2t+1 = 3d contiguous elements starting at
   // block row 2t (the zero row 0 is the left padding); + GELU + positional embedding -> residual x
@@ -257,22 +320,32 @@ void encode_chunk(wm_engine* e, const float* mel, long long ld, const int* h_see
     GemmA a{h1, 2LL * d, T, 3001LL * d};
     GemmEpi ep = epi_of(EPI_GELU_POS_F32, x, d, e->Wf("enc.conv2.b"));
     ep.rpb = T; ep.pos = e->Wf("enc.pos");
-    launch_gemm(a, e->Wb("enc.conv2.w"), 3LL * d, (int)M, d, 3 * d, ep, st);
+    gemm_p(e, P_ENC_GEMM, a, e->Wb("enc.conv2.w"), 3LL * d, (int)M, d, 3 * d, ep, st);
   }
   for (int l = 0; l < L; ++l) {
     const std::string p = "enc." + std::to_string(l) + ".";
-    launch_layernorm(x, d, nullptr, (int)M, d, e->Wf(p + "ln1.w"), e->Wf(p + "ln1.b"), hb, d, st);
-    launch_gemm(amat(hb, d), e->Wb(p + "qkv.w"), d, (int)M, 3 * d, d, epi_of(EPI_BF16, qkv, 3LL * d, e->Wf(p + "qkv.b")), st);
-    launch_attn_enc(qkv, ao, B, T, d, H, st);
-    launch_gemm(amat(ao, d), e->Wb(p + "out.w"), d, (int)M, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
-    launch_layernorm(x, d, nullptr, (int)M, d, e->Wf(p + "ln2.w"), e->Wf(p + "ln2.b"), hb, d, st);
+    {
+      ProfScope ps(e, P_ENC_OTHER, st);
+      launch_layernorm(x, d, nullptr, (int)M, d, e->Wf(p + "ln1.w"), e->Wf(p + "ln1.b"), hb, d, st);
+    }
+    gemm_p(e, P_ENC_GEMM, amat(hb, d), e->Wb(p + "qkv.w"), d, (int)M, 3 * d, d, epi_of(EPI_BF16, qkv, 3LL * d, e->Wf(p + "qkv.b")), st);
+    {
+      ProfScope ps(e, P_ENC_ATTN, st, 4.0 * B * (double)T * T * d, 2.0 * 4 * M * d);
+      launch_attn_enc(qkv, ao, B, T, d, H, st);
+    }
+    gemm_p(e, P_ENC_GEMM, amat(ao, d), e->Wb(p + "out.w"), d, (int)M, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
+    {
+      ProfScope ps(e, P_ENC_OTHER, st);
+      launch_layernorm(x, d, nullptr, (int)M, d, e->Wf(p + "ln2.w"), e->Wf(p + "ln2.b"), hb, d, st);
+    }
     {
       GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, e->Wf(p + "fc1.b"));
       ep.act = 1;
-      launch_gemm(amat(hb, d), e->Wb(p + "fc1.w"), d, (int)M, 4 * d, d, ep, st);
+      gemm_p(e, P_ENC_GEMM, amat(hb, d), e->Wb(p + "fc1.w"), d, (int)M, 4 * d, d, ep, st);
     }
-    launch_gemm(amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, (int)M, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
+    gemm_p(e, P_ENC_GEMM, amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, (int)M, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
   }
+  ProfScope ps(e, P_ENC_OTHER, st);
   launch_layernorm(x, d, nullptr, (int)M, d, e->Wf("enc.ln.w"), e->Wf("enc.ln.b"), out, d, st);
 }
 
@@ -319,22 +392,34 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
   bf16* skv = e->skv.as<bf16>();
   bf16* ckv = e->ckv.as<bf16>();
   const int splits = attn ? 1 : cross_splits(rows, H);
-  launch_embed(row_tok, row_pos, e->Wb("dec.embed"), e->Wf("dec.pos"), x, rows, d, st);
+  {
+    ProfScope ps(e, P_DEC_OTHER, st);
+    launch_embed(row_tok, row_pos, e->Wb("dec.embed"), e->Wf("dec.pos"), x, rows, d, st);
+  }
   for (int l = 0; l < L; ++l) {
     const std::string p = "dec." + std::to_string(l) + ".";
     bf16* kc = skv + (size_t)(2 * l) * skv_layer;
     bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
-    launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln1.w"), e->Wf(p + "ln1.b"), hb, d, st);
+    {
+      ProfScope ps(e, P_DEC_OTHER, st);
+      launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln1.w"), e->Wf(p + "ln1.b"), hb, d, st);
+    }
     {
       GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, e->Wf(p + "qkv.b"));
       ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
       ep.d = d; ep.n_head = H; ep.head_dim = 64; ep.n_ctx = C;
-      launch_gemm(amat(hb, d), e->Wb(p + "qkv.w"), d, rows, 3 * d, d, ep, st);
+      gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "qkv.w"), d, rows, 3 * d, d, ep, st);
     }
-    launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, st);
-    launch_gemm(amat(ao, d), e->Wb(p + "out.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
-    launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln2.w"), e->Wf(p + "ln2.b"), hb, d, st);
-    launch_gemm(amat(hb, d), e->Wb(p + "cq.w"), d, rows, d, d, epi_of(EPI_BF16, q, d, e->Wf(p + "cq.b")), st);
+    {
+      ProfScope ps(e, P_SELF_ATTN, st);
+      launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st);
+    }
+    gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "out.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
+    {
+      ProfScope ps(e, P_DEC_OTHER, st);
+      launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln2.w"), e->Wf(p + "ln2.b"), hb, d, st);
+    }
+    gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "cq.w"), d, rows, d, d, epi_of(EPI_BF16, q, d, e->Wf(p + "cq.b")), st);
     float* probs = nullptr;
     const int* hmap = nullptr;
     if (attn && align_map) {
@@ -347,21 +432,30 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
         hmap = e->d_head_map.as<int>();
       }
     }
-    launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
-                      e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, splits, e->s_pm.as<float>(),
-                      e->s_pl.as<float>(), e->s_po.as<float>(), probs, hmap, n_align, st);
+    {
+      ProfScope ps(e, P_CROSS_ATTN, st);
+      launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
+                        e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, splits, e->s_pm.as<float>(),
+                        e->s_pl.as<float>(), e->s_po.as<float>(), probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st);
+    }
     if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
-    launch_gemm(amat(ao, d), e->Wb(p + "cout.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "cout.b")), st);
-    launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln3.w"), e->Wf(p + "ln3.b"), hb, d, st);
+    gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "cout.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "cout.b")), st);
+    {
+      ProfScope ps(e, P_DEC_OTHER, st);
+      launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln3.w"), e->Wf(p + "ln3.b"), hb, d, st);
+    }
     {
       GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, e->Wf(p + "fc1.b"));
       ep.act = 1;
-      launch_gemm(amat(hb, d), e->Wb(p + "fc1.w"), d, rows, 4 * d, d, ep, st);
+      gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "fc1.w"), d, rows, 4 * d, d, ep, st);
     }
-    launch_gemm(amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
+    gemm_p(e, P_DEC_GEMM, amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
   }
-  launch_layernorm(x, d, logit_rows, n_logit, d, e->Wf("dec.ln.w"), e->Wf("dec.ln.b"), hb, d, st);
-  launch_gemm(amat(hb, d), e->Wb("dec.embed"), d, n_logit, m.n_vocab, d, epi_of(EPI_F32, logits, m.n_vocab, nullptr), st);
+  {
+    ProfScope ps(e, P_DEC_OTHER, st);
+    launch_layernorm(x, d, logit_rows, n_logit, d, e->Wf("dec.ln.w"), e->Wf("dec.ln.b"), hb, d, st);
+  }
+  gemm_p(e, P_LOGITS_GEMM, amat(hb, d), e->Wb("dec.embed"), d, n_logit, m.n_vocab, d, epi_of(EPI_F32, logits, m.n_vocab, nullptr), st);
 }
 
 void check_weights(wm_engine* e) {
@@ -498,6 +592,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
 
   auto select = [&](int step) {
     sp.step = step;
+    ProfScope ps(e, P_SELECT, st);
     launch_logits_select(sp, NH, st);
     if (beam) launch_beam_select(bp, W, st);
   };
@@ -677,7 +772,7 @@ void wm_destroy(wm_engine* e) {
                     &e->d_row_pos, &e->d_row_hyp, &e->d_hyp_slot, &e->d_n_active, &e->d_suppress, &e->d_cand_tok,
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
-                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po})
+                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->prof_dbytes})
     b->release();
   delete e;
 }
@@ -705,6 +800,7 @@ int wm_logmel(wm_engine* e, const float* d_pcm, int64_t pcm_offset, int64_t n_sa
               float* d_mel, int64_t ld, uint32_t* d_gmax, void* stream) {
   return guarded(e, [&] {
     const long long n_padded = n_samples + 160;
+    ProfScope ps(e, P_LOGMEL, (hipStream_t)stream, 2.0 * 201 * 400 * 2 * n_frames, 4.0 * 160 * n_frames + 4.0 * e->dm.n_mels * n_frames);
     launch_logmel(d_pcm, pcm_offset, n_samples, n_padded, frame0, n_frames, e->fe_window.as<float>(), e->fe_cos.as<float>(),
                   e->fe_sin.as<float>(), e->fe_filt.as<float>(), e->fe_lo.as<int>(), e->fe_hi.as<int>(), e->dm.n_mels,
                   d_mel, ld, d_gmax, (hipStream_t)stream);
@@ -761,7 +857,8 @@ int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void*
     const int d = m.n_state, T = m.n_audio_ctx;
     GemmEpi ep = epi_of(EPI_CROSS_KV, e->ckv.p, 0, e->Wf("dec.ckv.b"));
     ep.rpb = T; ep.d = d; ep.head_dim = 64; ep.n_head = m.n_head; ep.n_slots = e->n_slots; ep.slot0 = slot0;
-    launch_gemm(amat((const bf16*)d_enc, d), e->Wb("dec.ckv.w"), d, B * T, m.n_dec_layer * 2 * d, d, ep, (hipStream_t)stream);
+    gemm_p(e, P_CROSSKV_GEMM, amat((const bf16*)d_enc, d), e->Wb("dec.ckv.w"), d, B * T, m.n_dec_layer * 2 * d, d, ep,
+           (hipStream_t)stream);
   });
 }
 
@@ -777,5 +874,46 @@ int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_
 }
 
 int64_t wm_device_bytes(wm_engine* e) { return e ? (int64_t)e->device_bytes() : 0; }
+
+int32_t wm_profile_classes(void) { return P_N; }
+const char* wm_profile_name(int32_t cls) { return (cls >= 0 && cls < P_N) ? kProfNames[cls] : ""; }
+
+int wm_profile(wm_engine* e, int32_t enable) {
+  return guarded(e, [&] {
+    HIP_OK(hipDeviceSynchronize());
+    if (!enable) {            // stop recording; keep what was recorded for wm_profile_read
+      e->prof_on = false;
+      return;
+    }
+    for (int c = 0; c < P_N; ++c) {
+      for (auto& pr : e->prof_ev[c]) { e->ev_pool.push_back(pr.first); e->ev_pool.push_back(pr.second); }
+      e->prof_ev[c].clear();
+      e->prof_flops[c] = 0;
+      e->prof_bytes[c] = 0;
+    }
+    e->prof_dbytes.ensure(P_N * sizeof(unsigned long long));
+    HIP_OK(hipMemset(e->prof_dbytes.p, 0, P_N * sizeof(unsigned long long)));
+    e->prof_on = true;
+  });
+}
+
+int wm_profile_read(wm_engine* e, int32_t cls, int64_t* launches, double* ms, double* flops, double* bytes) {
+  return guarded(e, [&] {
+    if (cls < 0 || cls >= P_N) throw std::runtime_error("wm_profile_read: bad class");
+    HIP_OK(hipDeviceSynchronize());
+    double t = 0;
+    for (auto& pr : e->prof_ev[cls]) {
+      float x = 0;
+      HIP_OK(hipEventElapsedTime(&x, pr.first, pr.second));
+      t += x;
+    }
+    unsigned long long db[P_N] = {0};
+    if (e->prof_dbytes.p) HIP_OK(hipMemcpy(db, e->prof_dbytes.p, sizeof(db), hipMemcpyDeviceToHost));
+    *launches = (int64_t)e->prof_ev[cls].size();
+    *ms = t;
+    *flops = e->prof_flops[cls];
+    *bytes = e->prof_bytes[cls] + (double)db[cls];
+  });
+}
 
 }  // extern "C"

@@ -37,5 +37,6 @@ struct GemmEpi {
   int n_slots, slot0;
 };
 
-void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
-                 hipStream_t st);
+// ws: f32 scratch for split-K partial slabs (nullptr disables split-K)
+void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                 size_t ws_bytes, hipStream_t st);

@@ -134,6 +134,17 @@ class GpuEngine:
     def stream_ptr(self) -> C.c_void_p:
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def profile(self, enable: bool) -> None:
+        _capi.check(self.lib.wm_profile(self.h, int(enable)), "wm_profile")
+
+    def profile_read(self) -> Dict[str, dict]:
+        out = {}
+        for c in range(self.lib.wm_profile_classes()):
+            n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
+            _capi.check(self.lib.wm_profile_read(self.h, c, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by)), "wm_profile_read")
+            out[self.lib.wm_profile_name(c).decode()] = dict(launches=n.value, ms=ms.value, flops=fl.value, bytes=by.value)
+        return out
+
     def device_bytes(self) -> int:
         return int(self.lib.wm_device_bytes(self.h))
 

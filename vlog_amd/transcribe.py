@@ -1,0 +1,581 @@
+"""faster-whisper-shaped drop-in: WhisperModel(...).transcribe(...) -> (Iterable[Segment], TranscriptionInfo).
+
+This is the surface the vlog transcription worker calls (reference `worker/transcription.py:78-111`):
+
+    model = WhisperModel(WHISPER_MODEL, device="cpu", compute_type=TRANSCRIPTION_COMPUTE_TYPE)   # :81-85
+    segments, info = model.transcribe(str(wav), language=lang, task="transcribe", beam_size=5,
+                                      vad_filter=True)                                          # :105-111
+    for segment in segments: segment.start, segment.end, segment.text                           # :117-125
+    info.language                                                                               # :131
+
+Semantics follow faster-whisper 1.1.x `WhisperModel.transcribe` / `generate_segments` /
+`generate_with_fallback` / `add_word_timestamps` [FW↑] (restated; the package is not installed here):
+sequential seek loop over 30 s windows, previous-text prompt (`<|startofprev|>` + last 223 tokens),
+temperature fallback on compression ratio / average log-probability with the no-speech exemption, segment
+split at timestamp pairs, optional cross-attention word alignment.  Every tensor operation runs on the
+MI355X through libwhisper_mi355 (vlog_amd/engine.py); there is no CPU compute path: device="cpu" (the
+worker's literal argument) is remapped to the GPU and logged, and construction fails loudly when no GPU or
+no HIP library is available.
+
+`BatchedInferencePipeline` is the throughput mode (faster-whisper's class of the same name): fixed 30 s
+windows decoded independently (no text conditioning), batched on one GPU, or sharded over several GPUs
+with vlog_amd/shard.py.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import os
+import threading
+from dataclasses import asdict, dataclass, field
+from typing import BinaryIO, Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import segments as segs
+from .audio import load_audio
+from .dims import CHUNK_LENGTH, HOP_LENGTH, N_FRAMES, SAMPLE_RATE, TIME_PRECISION
+from .tokenizer import Tokenizer
+from .weights import resolve_model
+
+logger = logging.getLogger("vlog_amd")
+
+FRAMES_PER_SECOND = SAMPLE_RATE // HOP_LENGTH          # 100
+INPUT_STRIDE = 2
+TOKENS_PER_SECOND = SAMPLE_RATE // (HOP_LENGTH * INPUT_STRIDE)   # 50
+MAX_LENGTH = 448
+
+
+@dataclass
+class Word:
+    start: float
+    end: float
+    word: str
+    probability: float
+
+    def _asdict(self):
+        return asdict(self)
+
+
+@dataclass
+class Segment:
+    id: int
+    seek: int
+    start: float
+    end: float
+    text: str
+    tokens: List[int]
+    avg_logprob: float
+    compression_ratio: float
+    no_speech_prob: float
+    words: Optional[List[Word]]
+    temperature: Optional[float]
+
+    def _asdict(self):
+        return asdict(self)
+
+
+@dataclass
+class TranscriptionOptions:
+    beam_size: int
+    best_of: int
+    patience: float
+    length_penalty: float
+    repetition_penalty: float
+    no_repeat_ngram_size: int
+    log_prob_threshold: Optional[float]
+    no_speech_threshold: Optional[float]
+    compression_ratio_threshold: Optional[float]
+    condition_on_previous_text: bool
+    prompt_reset_on_temperature: float
+    temperatures: List[float]
+    initial_prompt: Optional[Union[str, Iterable[int]]]
+    prefix: Optional[str]
+    suppress_blank: bool
+    suppress_tokens: Optional[List[int]]
+    without_timestamps: bool
+    max_initial_timestamp: float
+    word_timestamps: bool
+    prepend_punctuations: str
+    append_punctuations: str
+    multilingual: bool
+    max_new_tokens: Optional[int]
+    clip_timestamps: Union[str, List[float]]
+    hallucination_silence_threshold: Optional[float]
+    hotwords: Optional[str]
+
+
+@dataclass
+class VadOptions:
+    threshold: float = 0.5
+    neg_threshold: Optional[float] = None
+    min_speech_duration_ms: int = 0
+    max_speech_duration_s: float = float("inf")
+    min_silence_duration_ms: int = 2000
+    speech_pad_ms: int = 400
+
+
+@dataclass
+class TranscriptionInfo:
+    language: str
+    language_probability: float
+    duration: float
+    duration_after_vad: float
+    all_language_probs: Optional[List[Tuple[str, float]]]
+    transcription_options: TranscriptionOptions
+    vad_options: Optional[VadOptions]
+
+
+@dataclass
+class _GenOut:
+    tokens: List[int]
+    score: float
+    no_speech_prob: float
+
+
+def _resolve_device_index(device: str, device_index) -> int:
+    if isinstance(device_index, (list, tuple)):
+        if len(device_index) != 1:
+            raise ValueError("one WhisperModel drives one GPU; use BatchedInferencePipeline(shards=...) or "
+                             "vlog_amd.shard for several")
+        device_index = device_index[0]
+    env = os.environ.get("VLOG_AMD_DEVICE")
+    if env is not None:
+        device_index = int(env)
+    if device in ("cpu", "auto", "cuda", "rocm", "hip"):
+        if device == "cpu":
+            logger.warning("WhisperModel(device='cpu') remapped to MI355X GPU %d (vlog_amd has no CPU path)", device_index)
+    else:
+        raise ValueError(f"unsupported device {device!r}")
+    if not torch.cuda.is_available():
+        raise RuntimeError("vlog_amd.WhisperModel needs an AMD Instinct GPU (torch.cuda.is_available() is False)")
+    return int(device_index)
+
+
+class WhisperModel:
+    """faster_whisper.WhisperModel-compatible constructor (model_size_or_path, device, device_index,
+    compute_type, cpu_threads, num_workers, download_root, local_files_only, files, revision, ...)."""
+
+    def __init__(self, model_size_or_path: str, device: str = "auto", device_index: Union[int, List[int]] = 0,
+                 compute_type: str = "default", cpu_threads: int = 0, num_workers: int = 1,
+                 download_root: Optional[str] = None, local_files_only: bool = False, files: dict = None,
+                 revision: Optional[str] = None, use_auth_token=None, seed: int = 0,
+                 eot_after: Optional[int] = None, **model_kwargs):
+        from .engine import GpuEngine
+
+        if files:
+            raise NotImplementedError("in-memory model files are not supported")
+        if compute_type not in ("default", "auto", "int8", "int8_float16", "int8_float32", "int8_bfloat16",
+                                "float16", "bfloat16", "float32"):
+            raise ValueError(f"unsupported compute_type {compute_type!r}")
+        if compute_type not in ("default", "auto", "bfloat16"):
+            logger.info("compute_type=%s mapped to bf16 weights / f32 accumulation on MI355X", compute_type)
+        self.device_index = _resolve_device_index(device, device_index)
+        self.dims, sd, model_dir = resolve_model(model_size_or_path, seed=seed, eot_after=eot_after)
+        self.model_dir = model_dir
+        tj = os.path.join(model_dir, "tokenizer.json") if model_dir else None
+        self._tokenizer_json = tj if tj and os.path.isfile(tj) else None
+        self._tok_seed = seed
+        self.engine = GpuEngine(self.dims, sd, self.device_index)
+        del sd
+        self.engine.reserve(1, 8)
+        self._lock = threading.Lock()
+        self.feature_size = self.dims.n_mels
+        self.num_samples_per_token = HOP_LENGTH * INPUT_STRIDE
+        self.frames_per_second = FRAMES_PER_SECOND
+        self.tokens_per_second = TOKENS_PER_SECOND
+        self.input_stride = INPUT_STRIDE
+        self.time_precision = TIME_PRECISION
+        self.max_length = MAX_LENGTH
+
+    @property
+    def is_multilingual(self) -> bool:
+        return self.dims.multilingual
+
+    @property
+    def supported_languages(self) -> List[str]:
+        return list(self.dims.specials.lang_codes) if self.is_multilingual else ["en"]
+
+    def tokenizer(self, task: Optional[str] = "transcribe", language: Optional[str] = None) -> Tokenizer:
+        return Tokenizer(self.dims, task=task, language=language, tokenizer_json=self._tokenizer_json, seed=self._tok_seed)
+
+    # ------------------------------------------------------------------ features / encoder
+    def _features(self, audio: np.ndarray) -> torch.Tensor:
+        return self.engine.features(torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)))
+
+    def _encode(self, features: torch.Tensor, seek: int, size: int, slot: int = 0) -> torch.Tensor:
+        enc = self.engine.encode(features, [seek], [size])
+        self.engine.cross_kv(enc, slot)
+        return enc
+
+    # ------------------------------------------------------------------ language detection
+    def detect_language(self, audio: Optional[np.ndarray] = None, features: Optional[torch.Tensor] = None,
+                        vad_filter: bool = False, vad_parameters=None, language_detection_segments: int = 1,
+                        language_detection_threshold: float = 0.5) -> Tuple[str, float, List[Tuple[str, float]]]:
+        """faster-whisper `detect_language`: encode up to `language_detection_segments` windows, one decoder
+        step from <|startoftranscript|>, softmax over the language tokens; majority vote if no window is
+        confident."""
+        if not self.is_multilingual:
+            return "en", 1.0, [("en", 1.0)]
+        with self._lock:
+            if features is None:
+                features = self._features(audio)
+            st = self.dims.specials
+            content = features.shape[1] - 1 if features.shape[1] > 1 else features.shape[1]
+            info = {}
+            all_probs: List[Tuple[str, float]] = []
+            lang, prob = "en", 0.0
+            n_seg = max(1, language_detection_segments)
+            for i in range(n_seg):
+                seek = i * N_FRAMES
+                if i > 0 and seek >= content:
+                    break
+                size = max(0, min(N_FRAMES, content - seek))
+                self._encode(features, seek, size, 0)
+                logits, _ = self.engine.forward([0], np.array([[st.sot]], dtype=np.int32), last_only=True)
+                lg = logits[0, st.lang_begin: st.lang_begin + st.n_langs].double()
+                p = torch.softmax(lg, dim=0).cpu().numpy()
+                order = np.argsort(-p, kind="stable")
+                all_probs = [(st.lang_codes[j], float(p[j])) for j in order]
+                lang, prob = all_probs[0]
+                if prob > language_detection_threshold:
+                    break
+                info.setdefault(lang, []).append(prob)
+            else:
+                lang = max(info, key=lambda k: len(info[k]))
+                prob = max(info[lang])
+            return lang, prob, all_probs
+
+    # ------------------------------------------------------------------ transcribe
+    def transcribe(self, audio: Union[str, BinaryIO, np.ndarray], language: Optional[str] = None,
+                   task: str = "transcribe", log_progress: bool = False, beam_size: int = 5, best_of: int = 5,
+                   patience: float = 1, length_penalty: float = 1, repetition_penalty: float = 1,
+                   no_repeat_ngram_size: int = 0,
+                   temperature: Union[float, List[float], Tuple[float, ...]] = (0.0, 0.2, 0.4, 0.6, 0.8, 1.0),
+                   compression_ratio_threshold: Optional[float] = 2.4, log_prob_threshold: Optional[float] = -1.0,
+                   no_speech_threshold: Optional[float] = 0.6, condition_on_previous_text: bool = True,
+                   prompt_reset_on_temperature: float = 0.5, initial_prompt: Optional[Union[str, Iterable[int]]] = None,
+                   prefix: Optional[str] = None, suppress_blank: bool = True, suppress_tokens: Optional[List[int]] = [-1],
+                   without_timestamps: bool = False, max_initial_timestamp: float = 1.0, word_timestamps: bool = False,
+                   prepend_punctuations: str = "\"'“¿([{-", append_punctuations: str = "\"'.。,，!！?？:：”)]}、",
+                   multilingual: bool = False, vad_filter: bool = False, vad_parameters=None,
+                   max_new_tokens: Optional[int] = None, chunk_length: Optional[int] = None,
+                   clip_timestamps: Union[str, List[float]] = "0", hallucination_silence_threshold: Optional[float] = None,
+                   hotwords: Optional[str] = None, language_detection_threshold: Optional[float] = 0.5,
+                   language_detection_segments: int = 1):
+        for name, val, default in (("repetition_penalty", repetition_penalty, 1), ("no_repeat_ngram_size", no_repeat_ngram_size, 0),
+                                   ("prefix", prefix, None), ("hotwords", hotwords, None), ("multilingual", multilingual, False),
+                                   ("hallucination_silence_threshold", hallucination_silence_threshold, None)):
+            if val != default:
+                raise NotImplementedError(f"{name}={val!r} is not supported by the MI355X engine")
+        if chunk_length not in (None, CHUNK_LENGTH):
+            raise NotImplementedError("chunk_length other than 30 s is not supported")
+        if task not in ("transcribe", "translate"):
+            raise ValueError(f"unknown task {task!r}")
+        if not isinstance(audio, np.ndarray):
+            audio = load_audio(audio)
+        audio = np.asarray(audio, dtype=np.float32)
+        duration = audio.shape[0] / SAMPLE_RATE
+        duration_after_vad = duration
+        speech_chunks = None
+        vad_opts = None
+        if vad_filter and clip_timestamps in ("0", [0], [0.0]):
+            from .vad import collect_chunks, get_speech_timestamps
+            vad_opts = vad_parameters if isinstance(vad_parameters, VadOptions) else VadOptions(**(vad_parameters or {}))
+            speech_chunks = get_speech_timestamps(audio, vad_opts, self)
+            audio = collect_chunks(audio, speech_chunks)
+            duration_after_vad = audio.shape[0] / SAMPLE_RATE
+
+        with self._lock:
+            features = self._features(audio)
+        all_language_probs = None
+        if language is None:
+            if not self.is_multilingual:
+                language, language_probability = "en", 1.0
+            else:
+                language, language_probability, all_language_probs = self.detect_language(
+                    features=features, language_detection_segments=language_detection_segments,
+                    language_detection_threshold=language_detection_threshold or 0.5)
+        else:
+            if not self.is_multilingual and language != "en":
+                logger.warning("English-only model used with language=%s; using 'en'", language)
+                language = "en"
+            language_probability = 1.0
+        tokenizer = self.tokenizer(task=task, language=language)
+        temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
+        options = TranscriptionOptions(
+            beam_size=beam_size, best_of=best_of, patience=patience, length_penalty=length_penalty,
+            repetition_penalty=repetition_penalty, no_repeat_ngram_size=no_repeat_ngram_size,
+            log_prob_threshold=log_prob_threshold, no_speech_threshold=no_speech_threshold,
+            compression_ratio_threshold=compression_ratio_threshold, condition_on_previous_text=condition_on_previous_text,
+            prompt_reset_on_temperature=prompt_reset_on_temperature, temperatures=temps, initial_prompt=initial_prompt,
+            prefix=prefix, suppress_blank=suppress_blank,
+            suppress_tokens=list(tokenizer.suppressed_tokens(suppress_tokens)) if suppress_tokens else [],
+            without_timestamps=without_timestamps, max_initial_timestamp=max_initial_timestamp,
+            word_timestamps=word_timestamps, prepend_punctuations=prepend_punctuations,
+            append_punctuations=append_punctuations, multilingual=multilingual, max_new_tokens=max_new_tokens,
+            clip_timestamps=clip_timestamps, hallucination_silence_threshold=hallucination_silence_threshold,
+            hotwords=hotwords)
+        gen = self.generate_segments(features, tokenizer, options)
+        if speech_chunks:
+            from .vad import restore_speech_timestamps
+            gen = restore_speech_timestamps(gen, speech_chunks, SAMPLE_RATE)
+        info = TranscriptionInfo(language=language, language_probability=language_probability, duration=duration,
+                                 duration_after_vad=duration_after_vad, all_language_probs=all_language_probs,
+                                 transcription_options=options, vad_options=vad_opts)
+        return gen, info
+
+    # ------------------------------------------------------------------ prompt / generate
+    def get_prompt(self, tokenizer: Tokenizer, previous_tokens: List[int], without_timestamps: bool = False) -> List[int]:
+        prompt: List[int] = []
+        if previous_tokens:
+            prompt.append(tokenizer.sot_prev)
+            prompt.extend(previous_tokens[-(self.max_length // 2 - 1):])
+        prompt.extend(tokenizer.sot_sequence)
+        if without_timestamps:
+            prompt.append(tokenizer.no_timestamps)
+        return prompt
+
+    def _generate(self, prompt: List[int], options: TranscriptionOptions, temperature: float, max_length: int,
+                  seed: int) -> _GenOut:
+        st = self.dims.specials
+        mit = int(round(options.max_initial_timestamp / self.time_precision))
+        sampling = temperature > 0
+        res, _ = self.engine.generate(
+            [0], [prompt], beam_size=1 if sampling else options.beam_size, patience=options.patience,
+            length_penalty=options.length_penalty, max_length=max_length, temperature=temperature,
+            num_hypotheses=options.best_of if sampling else 1, seed=seed, suppress_tokens=options.suppress_tokens,
+            suppress_blank=options.suppress_blank, max_initial_timestamp_index=mit,
+            with_timestamps=not options.without_timestamps,
+            sot_index=prompt.index(st.sot) if st.sot in prompt else -1, check_every=4)
+        r = res[0]
+        return _GenOut(r.tokens, r.score, r.no_speech_prob)
+
+    def generate_with_fallback(self, prompt: List[int], tokenizer: Tokenizer, options: TranscriptionOptions,
+                               seed: int = 0):
+        """faster-whisper generate_with_fallback -> (result, avg_logprob, temperature, compression_ratio)."""
+        all_results, below_cr = [], []
+        if options.max_new_tokens is not None:
+            max_length = len(prompt) + options.max_new_tokens
+        else:
+            max_length = self.max_length
+        if max_length > self.max_length:
+            raise ValueError(f"the length of the prompt is {len(prompt)}, and the max_new_tokens {max_length - len(prompt)}. "
+                             f"Thus, the combined length of the prompt and max_new_tokens is: {max_length}. This exceeds "
+                             f"the max_length of the Whisper model: {self.max_length}.")
+        decode_result = None
+        temperature = options.temperatures[0] if options.temperatures else 0.0
+        for i, temperature in enumerate(options.temperatures):
+            result = self._generate(prompt, options, temperature, max_length, seed + i)
+            n = len(result.tokens)
+            avg_lp = segs.avg_logprob(result.score, n, options.length_penalty)
+            text = tokenizer.decode(result.tokens).strip()
+            cr = segs.compression_ratio(text)
+            decode_result = (result, avg_lp, temperature, cr)
+            all_results.append(decode_result)
+            fb, below = segs.needs_fallback(cr, avg_lp, result.no_speech_prob, options.compression_ratio_threshold,
+                                            options.log_prob_threshold, options.no_speech_threshold)
+            if below:
+                below_cr.append(decode_result)
+            if not fb:
+                break
+        else:
+            best = max(below_cr or all_results, key=lambda x: x[1])
+            decode_result = (best[0], best[1], temperature, best[3])
+        return decode_result
+
+    # ------------------------------------------------------------------ seek loop
+    def generate_segments(self, features: torch.Tensor, tokenizer: Tokenizer, options: TranscriptionOptions):
+        content_frames = features.shape[1] - 1
+        ct = options.clip_timestamps
+        if isinstance(ct, str):
+            ct = [float(t) for t in (ct.split(",") if ct else [])]
+        seek_points = [round(t * self.frames_per_second) for t in ct]
+        if not seek_points:
+            seek_points.append(0)
+        if len(seek_points) % 2 == 1:
+            seek_points.append(content_frames)
+        seek_clips = list(zip(seek_points[::2], seek_points[1::2]))
+        idx = 0
+        clip_idx = 0
+        seek = seek_clips[0][0]
+        all_tokens: List[int] = []
+        prompt_reset_since = 0
+        if options.initial_prompt is not None:
+            if isinstance(options.initial_prompt, str):
+                all_tokens.extend(tokenizer.encode(" " + options.initial_prompt.strip()))
+            else:
+                all_tokens.extend(options.initial_prompt)
+        last_speech_timestamp = 0.0
+        window = 0
+        while clip_idx < len(seek_clips):
+            clip_start, clip_end = seek_clips[clip_idx]
+            clip_end = min(clip_end, content_frames)
+            if seek < clip_start:
+                seek = clip_start
+            if seek >= clip_end:
+                clip_idx += 1
+                if clip_idx < len(seek_clips):
+                    seek = seek_clips[clip_idx][0]
+                continue
+            time_offset = seek * HOP_LENGTH / SAMPLE_RATE
+            segment_size = min(N_FRAMES, content_frames - seek, clip_end - seek)
+            segment_duration = segment_size * HOP_LENGTH / SAMPLE_RATE
+            previous_tokens = all_tokens[prompt_reset_since:]
+            with self._lock:
+                self._encode(features, seek, segment_size, 0)
+                prompt = self.get_prompt(tokenizer, previous_tokens, options.without_timestamps)
+                result, avg_lp, temperature, cr = self.generate_with_fallback(prompt, tokenizer, options, seed=window)
+            window += 1
+            if segs.should_skip_window(result.no_speech_prob, avg_lp, options.no_speech_threshold, options.log_prob_threshold):
+                seek += segment_size
+                continue
+            tokens = result.tokens
+            previous_seek = seek
+            current, seek, single_ending = segs.split_segments_by_timestamps(
+                tokens, tokenizer.timestamp_begin, time_offset, segment_size, segment_duration, seek)
+            if options.word_timestamps:
+                with self._lock:
+                    last_speech_timestamp = self.add_word_timestamps(
+                        [current], tokenizer, segment_size, options.prepend_punctuations, options.append_punctuations,
+                        last_speech_timestamp)
+                if not single_ending:
+                    last_word_end = _get_end(current)
+                    if last_word_end is not None and last_word_end > time_offset:
+                        seek = round(last_word_end * self.frames_per_second)
+            for s in current:
+                text = tokenizer.decode(s["tokens"])
+                if s["start"] == s["end"] or not text.strip():
+                    continue
+                all_tokens.extend(s["tokens"])
+                idx += 1
+                yield Segment(id=idx, seek=previous_seek, start=s["start"], end=s["end"], text=text,
+                              tokens=s["tokens"], temperature=temperature, avg_logprob=avg_lp, compression_ratio=cr,
+                              no_speech_prob=result.no_speech_prob,
+                              words=[Word(**w) for w in s["words"]] if options.word_timestamps else None)
+            if not options.condition_on_previous_text or temperature > options.prompt_reset_on_temperature:
+                prompt_reset_since = len(all_tokens)
+
+    # ------------------------------------------------------------------ word timestamps
+    def find_alignment(self, tokenizer: Tokenizer, text_tokens: List[List[int]], num_frames: int,
+                       median_filter_width: int = 7, slot: int = 0) -> List[List[dict]]:
+        """faster-whisper find_alignment over CTranslate2 align: teacher-forced decoder pass over
+        [sot_sequence, <|notimestamps|>, text, <|endoftext|>] with the alignment heads' cross-attention
+        captured on the GPU, normalise + median filter + DTW on the GPU (vlog_amd/align.py)."""
+        from .align import align_tokens
+        out = []
+        for tt in text_tokens:
+            if not tt:
+                out.append([])
+                continue
+            probs, text_idx, time_idx = align_tokens(self.engine, self.dims, tokenizer, tt, num_frames,
+                                                     median_filter_width, slot)
+            words, word_tokens = tokenizer.split_to_word_tokens(tt + [tokenizer.eot])
+            if len(word_tokens) <= 1:
+                out.append([])
+                continue
+            wb = np.pad(np.cumsum([len(t) for t in word_tokens[:-1]]), (1, 0))
+            if len(wb) <= 1:
+                out.append([])
+                continue
+            jumps = np.pad(np.diff(text_idx), (1, 0), constant_values=1).astype(bool)
+            jump_times = time_idx[jumps] / self.tokens_per_second
+            starts = jump_times[wb[:-1]]
+            ends = jump_times[wb[1:]]
+            wprob = [float(np.mean(probs[i:j])) for i, j in zip(wb[:-1], wb[1:])]
+            out.append([dict(word=w, tokens=t, start=float(s), end=float(e), probability=p)
+                        for w, t, s, e, p in zip(words, word_tokens, starts, ends, wprob)])
+        return out
+
+    def add_word_timestamps(self, segments: List[List[dict]], tokenizer: Tokenizer, num_frames: int,
+                            prepend_punctuations: str, append_punctuations: str, last_speech_timestamp: float) -> float:
+        if len(segments) == 0:
+            return last_speech_timestamp
+        text_tokens, per_seg = [], []
+        for segment in segments:
+            st = [[t for t in sub["tokens"] if t < tokenizer.eot] for sub in segment]
+            text_tokens.append(list(itertools.chain.from_iterable(st)))
+            per_seg.append(st)
+        alignments = self.find_alignment(tokenizer, text_tokens, num_frames)
+        med_max = []
+        for alignment in alignments:
+            durs = np.array([w["end"] - w["start"] for w in alignment])
+            durs = durs[durs.nonzero()]
+            med = min(0.7, float(np.median(durs))) if len(durs) > 0 else 0.0
+            mx = med * 2
+            if len(durs) > 0:
+                marks = ".。!！?？"
+                for i in range(1, len(alignment)):
+                    if alignment[i]["end"] - alignment[i]["start"] > mx:
+                        if alignment[i]["word"] in marks:
+                            alignment[i]["end"] = alignment[i]["start"] + mx
+                        elif alignment[i - 1]["word"] in marks:
+                            alignment[i]["start"] = alignment[i]["end"] - mx
+            merge_punctuations(alignment, prepend_punctuations, append_punctuations)
+            med_max.append((med, mx))
+        for si, segment in enumerate(segments):
+            wi = 0
+            time_offset = segment[0]["seek"] / self.frames_per_second
+            med, mx = med_max[si]
+            for ssi, sub in enumerate(segment):
+                saved = 0
+                words = []
+                while wi < len(alignments[si]) and saved < len(per_seg[si][ssi]):
+                    timing = alignments[si][wi]
+                    if timing["word"]:
+                        words.append(dict(word=timing["word"], start=round(time_offset + timing["start"], 2),
+                                          end=round(time_offset + timing["end"], 2), probability=timing["probability"]))
+                    saved += len(timing["tokens"])
+                    wi += 1
+                if words:
+                    if words[0]["end"] - last_speech_timestamp > med * 4 and (
+                            words[0]["end"] - words[0]["start"] > mx
+                            or (len(words) > 1 and words[1]["end"] - words[0]["start"] > mx * 2)):
+                        if len(words) > 1 and words[1]["end"] - words[1]["start"] > mx:
+                            boundary = max(words[1]["end"] / 2, words[1]["end"] - mx)
+                            words[0]["end"] = words[1]["start"] = boundary
+                        words[0]["start"] = max(0, words[0]["end"] - mx)
+                    if sub["start"] < words[0]["end"] and sub["start"] - 0.5 > words[0]["start"]:
+                        words[0]["start"] = max(0, min(words[0]["end"] - med, sub["start"]))
+                    else:
+                        sub["start"] = words[0]["start"]
+                    if sub["end"] > words[-1]["start"] and sub["end"] + 0.5 < words[-1]["end"]:
+                        words[-1]["end"] = max(words[-1]["start"] + med, sub["end"])
+                    else:
+                        sub["end"] = words[-1]["end"]
+                    last_speech_timestamp = sub["end"]
+                segments[si][ssi]["words"] = words
+        return last_speech_timestamp
+
+
+def _get_end(segments: List[dict]) -> Optional[float]:
+    return next((w["end"] for s in reversed(segments) for w in reversed(s.get("words") or [])),
+                segments[-1]["end"] if segments else None)
+
+
+def merge_punctuations(alignment: List[dict], prepended: str, appended: str) -> None:
+    """faster-whisper / openai merge_punctuations."""
+    i = len(alignment) - 2
+    j = len(alignment) - 1
+    while i >= 0:
+        prev, foll = alignment[i], alignment[j]
+        if prev["word"].startswith(" ") and prev["word"].strip() in prepended:
+            foll["word"] = prev["word"] + foll["word"]
+            foll["tokens"] = prev["tokens"] + foll["tokens"]
+            prev["word"] = ""
+            prev["tokens"] = []
+        else:
+            j = i
+        i -= 1
+    i, j = 0, 1
+    while j < len(alignment):
+        prev, foll = alignment[i], alignment[j]
+        if not prev["word"].endswith(" ") and foll["word"] in appended:
+            prev["word"] = prev["word"] + foll["word"]
+            prev["tokens"] = prev["tokens"] + foll["tokens"]
+            foll["word"] = ""
+            foll["tokens"] = []
+        else:
+            i = j
+        j += 1

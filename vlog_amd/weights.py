@@ -99,18 +99,40 @@ def synthetic_state_dict(dims: ModelDims, seed: int = 0, eot_after: Optional[int
     return sd
 
 
+# Final decoder residual-stream std of the seeded random init, by decoder depth (measured with the oracle on
+# teacher-forced sequences; used to scale the planted <|endoftext|> ramp to the model's depth).
+_RESID_STD = {4: 0.41, 6: 0.67, 12: 1.50, 24: 2.94, 32: 4.5}
+
+
+def _resid_std(n_layers: int) -> float:
+    ks = sorted(_RESID_STD)
+    if n_layers in _RESID_STD:
+        return _RESID_STD[n_layers]
+    lo = max([k for k in ks if k <= n_layers], default=ks[0])
+    hi = min([k for k in ks if k >= n_layers], default=ks[-1])
+    if lo == hi:
+        return _RESID_STD[lo] * n_layers / lo
+    t = (n_layers - lo) / (hi - lo)
+    return _RESID_STD[lo] * (1 - t) + _RESID_STD[hi] * t
+
+
+EOT_KAPPA = 4.0
+
+
 def plant_eot(sd: Dict[str, torch.Tensor], dims: ModelDims, eot_after: int, seed: int = 0) -> None:
-    """Plant one direction u: decoder position p carries (0.0084 / eot_after) * p * sqrt(d) * u and
-    E[<|endoftext|>] = 0.1 * sqrt(d) * u, so the <|endoftext|> logit grows with position and greedy decoding
-    ends after about `eot_after` tokens (slope calibrated on tiny with the oracle: 84 tokens at 100)."""
+    """Plant one direction u: E[<|endoftext|>] = c_e * u (the norm of a random row) and decoder position p
+    carries slope * p * u with slope = EOT_KAPPA * s_L / (c_e * eot_after) (s_L = final residual std for this
+    decoder depth), so the <|endoftext|> logit rises by about EOT_KAPPA over `eot_after` positions and
+    greedy decoding ends near there."""
     d = dims.n_state
     g = _gen(seed, "plant_eot")
     u = torch.randn(d, generator=g)
     u = u / u.norm()
     pos = sd["model.decoder.embed_positions.weight"]
-    slope = 0.0084 / float(eot_after) * float(np.sqrt(d))
+    c_e = 0.02 * float(np.sqrt(d))            # same norm as any random embedding row
+    slope = EOT_KAPPA * _resid_std(dims.n_dec_layer) / (c_e * float(eot_after))
     pos += slope * torch.arange(pos.shape[0], dtype=torch.float32)[:, None] * u[None, :]
-    sd["model.decoder.embed_tokens.weight"][dims.specials.eot] = 0.1 * float(np.sqrt(d)) * u
+    sd["model.decoder.embed_tokens.weight"][dims.specials.eot] = c_e * u
 
 
 def round_bf16(sd: Dict[str, torch.Tensor]) -> Dict[str, np.ndarray]:
