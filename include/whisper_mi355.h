@@ -52,6 +52,10 @@ int wm_logmel(wm_engine* e, const float* d_pcm, int64_t pcm_offset, int64_t n_sa
 int wm_logmel_finalize(wm_engine* e, float* d_mel, int64_t n_frames, int64_t ld, const uint32_t* d_gmax,
                        const float* h_gmax, float* h_gmax_out, void* stream);
 
+/* Per-frame log energy (dB) of ceil(n_samples / frame) frames, the speech-probability input of the VAD
+ * stand-in (faster-whisper's Silero VAD [FW↑], reached via vad_filter=True at worker/transcription.py:110). */
+int wm_frame_energy(wm_engine* e, const float* d_pcm, int64_t n_samples, int32_t frame, float* d_db, void* stream);
+
 /* Encoder, replacing ctranslate2 Whisper.encode(features) [FW↑] (faster-whisper generate_segments).
  * Window b reads mel frames [h_seek[b], h_seek[b]+h_nframes[b]) of d_mel (ld = frames per mel row) and
  * zero-pads to 3000 frames (faster-whisper pad_or_trim).  Output bf16 [B][1500][n_state]. */
@@ -106,6 +110,19 @@ int wm_generate(wm_engine* e, const wm_generate_args* a, void* stream);
 int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_len, const int32_t* h_tokens,
                float* d_logits, int32_t last_only, const int32_t* h_align_heads, int32_t n_align, float* d_attn,
                void* stream);
+
+/* ctranslate2 Whisper.align(encoder_output, start_sequence, text_tokens, num_frames, median_filter_width)
+ * [FW↑] for ONE window (faster-whisper find_alignment, word_timestamps=True): teacher-forced decoder pass over
+ * h_sot + <|notimestamps|> + h_text + <|endoftext|> with the n_heads (layer, head) alignment heads'
+ * cross-attention captured, text-token probabilities, z-score + median filter + head mean, DTW on the
+ * device.  Outputs: h_probs[n_text], the DTW path (h_text_idx, h_time_idx) of *h_path_len entries
+ * (capacity n_text + 1 + num_frames/2). */
+int wm_align(wm_engine* e, int32_t slot, int32_t sot_len, const int32_t* h_sot, int32_t n_text, const int32_t* h_text,
+             int32_t num_frames, const int32_t* h_heads, int32_t n_heads, int32_t median_filter_width, float* h_probs,
+             int32_t* h_text_idx, int32_t* h_time_idx, int32_t* h_path_len, void* stream);
+/* DTW alone on a device cost matrix d_cost[n][m] (openai dtw semantics); path as for wm_align. */
+int wm_dtw(wm_engine* e, const float* d_cost, int32_t n, int32_t m, int32_t* h_text_idx, int32_t* h_time_idx,
+           int32_t* h_path_len, void* stream);
 
 /* Bytes of device memory held by the engine (weights + caches + scratch). */
 int64_t wm_device_bytes(wm_engine* e);

@@ -1,0 +1,169 @@
+// Word alignment (word_timestamps=True) for gfx950: CTranslate2 Whisper.align's post-processing [FW↑]
+// (oracle: oracle/align.py; DTW and median filter pinned against transformers).
+//   token_probs_kernel  : softmax over the text vocabulary [0, eot) at each position -> prob of the next token
+//   align_norm_kernel   : per (head, frame) column: crop to num_frames/2 keys + renormalise each row,
+//                         z-score over the token axis                       -> z[h][r][f]
+//   align_median_kernel : per (row, frame): width-w reflect median along time, mean over heads, negate
+//   dtw_kernel          : one workgroup per matrix, anti-diagonal wavefront over the (N+1) x (F+1) cost grid
+//                         (cells of one diagonal are independent), then a single-lane backtrace.
+#include "common.h"
+#include <stdexcept>
+#include <string>
+
+__global__ __launch_bounds__(256) void token_probs_kernel(const float* __restrict__ logits, int V, int eot,
+                                                          const int* __restrict__ next_tok, float* __restrict__ out) {
+  __shared__ float red[4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* lg = logits + (long long)r * V;
+  float m = -INFINITY;
+  for (int i = tid; i < eot; i += 256) m = fmaxf(m, lg[i]);
+  m = wave_max(m);
+  if (lane == 0) red[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int i = tid; i < eot; i += 256) s += expf(lg[i] - m);
+  s = wave_sum(s);
+  if (lane == 0) red[wv] = s;
+  __syncthreads();
+  if (tid == 0) {
+    s = red[0] + red[1] + red[2] + red[3];
+    out[r] = expf(lg[next_tok[r]] - m) / s;
+  }
+}
+
+// attn layout [S][n_heads][T]; rows r in [0, S); z layout [n_heads][S][F]
+__global__ void align_norm_kernel(const float* __restrict__ attn, int S, int nh, int T, int F, float* __restrict__ rowsum,
+                                  float* __restrict__ z) {
+  const int h = blockIdx.y;
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  double mean = 0.0, m2 = 0.0;
+  for (int r = 0; r < S; ++r) {
+    const double w = (double)attn[((long long)r * nh + h) * T + f] / (double)rowsum[r * nh + h];
+    mean += w;
+    m2 += w * w;
+  }
+  mean /= S;
+  const double var = fmax(m2 / S - mean * mean, 0.0);
+  const double inv = 1.0 / sqrt(var);
+  for (int r = 0; r < S; ++r) {
+    const double w = (double)attn[((long long)r * nh + h) * T + f] / (double)rowsum[r * nh + h];
+    z[((long long)h * S + r) * F + f] = (float)((w - mean) * inv);
+  }
+}
+
+__global__ void align_rowsum_kernel(const float* __restrict__ attn, int S, int nh, int T, int F, float* __restrict__ rowsum) {
+  const int rh = blockIdx.x;     // r * nh + h
+  float s = 0.f;
+  for (int f = threadIdx.x; f < F; f += 64) s += attn[(long long)rh * T + f];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) rowsum[rh] = s;
+}
+
+#define MEDW_MAX 15
+__global__ void align_median_kernel(const float* __restrict__ z, int S, int nh, int F, int width, int r0, int nrows,
+                                    float* __restrict__ mat) {
+  const int r = blockIdx.y;          // output row: token row r0 + r
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F || r >= nrows) return;
+  const int pad = width / 2;
+  float acc = 0.f;
+  for (int h = 0; h < nh; ++h) {
+    const float* row = z + ((long long)h * S + r0 + r) * F;
+    float v;
+    if (F <= pad) {
+      v = row[f];
+    } else {
+      float win[MEDW_MAX];
+      for (int k = 0; k < width; ++k) {
+        int idx = f - pad + k;
+        if (idx < 0) idx = -idx;
+        if (idx >= F) idx = 2 * (F - 1) - idx;
+        win[k] = row[idx];
+      }
+      for (int a = 1; a < width; ++a) {            // insertion sort (width <= 15)
+        const float t = win[a];
+        int b = a - 1;
+        while (b >= 0 && win[b] > t) { win[b + 1] = win[b]; --b; }
+        win[b + 1] = t;
+      }
+      v = win[pad];
+    }
+    acc += v;
+  }
+  mat[(long long)r * F + f] = -(acc / nh);
+}
+
+// cost [(N+1)][(M+1)] f32, trace [(N+1)][(M+1)] int8 scratch; x [N][M]; out path (text, time) reversed order fixed
+__global__ __launch_bounds__(256) void dtw_kernel(const float* __restrict__ x, int N, int M, float* __restrict__ cost,
+                                                  signed char* __restrict__ trace, int* __restrict__ out_i,
+                                                  int* __restrict__ out_j, int* __restrict__ out_len) {
+  const int tid = threadIdx.x;
+  const long long W = M + 1;
+  for (long long k = tid; k < (long long)(N + 1) * W; k += 256) {
+    cost[k] = INFINITY;
+    trace[k] = -1;
+  }
+  __syncthreads();
+  if (tid == 0) cost[0] = 0.f;
+  __syncthreads();
+  // anti-diagonals d = i + j, i in [1, N], j in [1, M]
+  for (int d = 2; d <= N + M; ++d) {
+    const int i_lo = max(1, d - M), i_hi = min(N, d - 1);
+    for (int i = i_lo + tid; i <= i_hi; i += 256) {
+      const int j = d - i;
+      const float c0 = cost[(i - 1) * W + (j - 1)], c1 = cost[(i - 1) * W + j], c2 = cost[i * W + (j - 1)];
+      float c;
+      signed char t;
+      if (c0 < c1 && c0 < c2) { c = c0; t = 0; }
+      else if (c1 < c0 && c1 < c2) { c = c1; t = 1; }
+      else { c = c2; t = 2; }
+      cost[i * W + j] = x[(long long)(i - 1) * M + (j - 1)] + c;
+      trace[i * W + j] = t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int i = N, j = M, n = 0;
+    while (i > 0 || j > 0) {
+      out_i[n] = i - 1;
+      out_j[n] = j - 1;
+      ++n;
+      const signed char t = (i == 0) ? 2 : (j == 0) ? 1 : trace[i * W + j];
+      if (t == 0) { --i; --j; }
+      else if (t == 1) { --i; }
+      else { --j; }
+    }
+    // reverse in place
+    for (int a = 0, b = n - 1; a < b; ++a, --b) {
+      int ti = out_i[a]; out_i[a] = out_i[b]; out_i[b] = ti;
+      int tj = out_j[a]; out_j[a] = out_j[b]; out_j[b] = tj;
+    }
+    *out_len = n;
+  }
+}
+
+void launch_token_probs(const float* logits, int rows, int V, int eot, const int* next_tok, float* out, hipStream_t st) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(token_probs_kernel, dim3(rows), dim3(256), 0, st, logits, V, eot, next_tok, out);
+  WM_LAUNCH_CHECK("token_probs_kernel");
+}
+
+void launch_align_matrix(const float* attn, int S, int nh, int T, int F, int width, int r0, int nrows, float* rowsum,
+                         float* z, float* mat, hipStream_t st) {
+  if (width > MEDW_MAX || width % 2 != 1) throw std::runtime_error("median filter width must be odd and <= 15");
+  hipLaunchKernelGGL(align_rowsum_kernel, dim3(S * nh), dim3(64), 0, st, attn, S, nh, T, F, rowsum);
+  WM_LAUNCH_CHECK("align_rowsum_kernel");
+  hipLaunchKernelGGL(align_norm_kernel, dim3((F + 127) / 128, nh), dim3(128), 0, st, attn, S, nh, T, F, rowsum, z);
+  WM_LAUNCH_CHECK("align_norm_kernel");
+  hipLaunchKernelGGL(align_median_kernel, dim3((F + 127) / 128, nrows), dim3(128), 0, st, z, S, nh, F, width, r0, nrows, mat);
+  WM_LAUNCH_CHECK("align_median_kernel");
+}
+
+void launch_dtw(const float* x, int N, int M, float* cost, signed char* trace, int* out_i, int* out_j, int* out_len,
+                hipStream_t st) {
+  hipLaunchKernelGGL(dtw_kernel, dim3(1), dim3(256), 0, st, x, N, M, cost, trace, out_i, out_j, out_len);
+  WM_LAUNCH_CHECK("dtw_kernel");
+}

@@ -27,16 +27,21 @@ void launch_logmel(const float*, long long, long long, long long, long long, int
                    const float*, const float*, const int*, const int*, int, float*, long long, unsigned int*, hipStream_t);
 void launch_logmel_clamp(float*, long long, long long, long long, const unsigned int*, const float*, hipStream_t);
 void launch_ordered_to_float(const unsigned int*, float*, hipStream_t);
+void launch_frame_energy(const float*, long long, int, int, float*, hipStream_t);
 void launch_layernorm(const float*, long long, const int*, int, int, const float*, const float*, bf16*, long long, hipStream_t);
 void launch_embed(const int*, const int*, const bf16*, const float*, float*, int, int, hipStream_t);
 void launch_im2col_conv1(const float*, long long, const int*, const int*, int, int, int, bf16*, hipStream_t);
 void launch_zero_pad_rows(bf16*, int, long long, int, hipStream_t);
 void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
 void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const int*, const int*, const int*, const int*,
-                      bf16*, long long, int, int, int, unsigned long long*, hipStream_t);
+                      bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
                        long long, int, int, int, float*, float*, float*, float*, const int*, int, unsigned long long*,
-                       hipStream_t);
+                       hipStream_t, hipEvent_t, hipEvent_t);
+
+void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
+void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
+void launch_dtw(const float*, int, int, float*, signed char*, int*, int*, int*, hipStream_t);
 
 // Kernel classes timed by the built-in profiler (wm_profile / wm_profile_read).
 enum ProfClass {
@@ -111,6 +116,7 @@ struct wm_engine {
   std::vector<hipEvent_t> ev_pool;
   double prof_flops[P_N] = {0}, prof_bytes[P_N] = {0};
   DevBuf gemm_ws;            // split-K partial slabs
+  DevBuf a_logits, a_attn, a_next, a_probs, a_rowsum, a_z, a_mat, a_cost, a_trace, a_pi, a_pj, a_plen;
   DevBuf prof_dbytes;        // device counters (attention kernels add the bytes they actually read)
   hipEvent_t ev_get() {
     if (ev_pool.empty()) {
@@ -243,22 +249,27 @@ GemmEpi epi_of(int kind, void* out, long long ldc, const float* bias) {
 }
 GemmA amat(const bf16* ptr, long long ld) { return GemmA{ptr, ld, 0, 0}; }
 
+// Times one kernel class.  Plain mode records events around the launches; `attached` mode hands the two
+// events to a launcher that attaches them to the dispatch itself (hipExtLaunchKernelGGL), which times the
+// kernel alone (what rocprofv3 reports) instead of kernel + event-record overhead.
 struct ProfScope {
   wm_engine* e;
   int cls;
   hipStream_t st;
-  hipEvent_t a = nullptr;
-  ProfScope(wm_engine* e_, int cls_, hipStream_t st_, double flops = 0, double bytes = 0) : e(e_), cls(cls_), st(st_) {
+  bool attached;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(wm_engine* e_, int cls_, hipStream_t st_, double flops = 0, double bytes = 0, bool attached_ = false)
+      : e(e_), cls(cls_), st(st_), attached(attached_) {
     if (!e->prof_on) return;
     a = e->ev_get();
-    HIP_OK(hipEventRecord(a, st));
+    b = e->ev_get();
+    if (!attached) HIP_OK(hipEventRecord(a, st));
     e->prof_flops[cls] += flops;
     e->prof_bytes[cls] += bytes;
   }
   ~ProfScope() {
     if (!a) return;
-    hipEvent_t b = e->ev_get();
-    (void)hipEventRecord(b, st);
+    if (!attached) (void)hipEventRecord(b, st);
     e->prof_ev[cls].push_back({a, b});
   }
 };
@@ -411,8 +422,8 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
       gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "qkv.w"), d, rows, 3 * d, d, ep, st);
     }
     {
-      ProfScope ps(e, P_SELF_ATTN, st);
-      launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st);
+      ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
+      launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
     }
     gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "out.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
     {
@@ -433,10 +444,11 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
       }
     }
     {
-      ProfScope ps(e, P_CROSS_ATTN, st);
+      ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, splits == 1);
       launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
                         e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, splits, e->s_pm.as<float>(),
-                        e->s_pl.as<float>(), e->s_po.as<float>(), probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st);
+                        e->s_pl.as<float>(), e->s_po.as<float>(), probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st,
+                        splits == 1 ? ps.a : nullptr, splits == 1 ? ps.b : nullptr);
     }
     if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
     gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "cout.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "cout.b")), st);
@@ -716,6 +728,56 @@ void forward(wm_engine* e, int n_seq, const int* h_slots, int S, const int* h_to
   HIP_OK(hipStreamSynchronize(st));
 }
 
+void dtw_run(wm_engine* e, const float* d_x, int N, int M, int* h_i, int* h_j, int* h_len, hipStream_t st) {
+  e->a_cost.ensure((size_t)(N + 1) * (M + 1) * 4);
+  e->a_trace.ensure((size_t)(N + 1) * (M + 1));
+  e->a_pi.ensure((size_t)(N + M + 2) * 4);
+  e->a_pj.ensure((size_t)(N + M + 2) * 4);
+  e->a_plen.ensure(4);
+  launch_dtw(d_x, N, M, e->a_cost.as<float>(), e->a_trace.as<signed char>(), e->a_pi.as<int>(), e->a_pj.as<int>(),
+             e->a_plen.as<int>(), st);
+  int n = 0;
+  HIP_OK(hipMemcpyAsync(&n, e->a_plen.p, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipMemcpyAsync(h_i, e->a_pi.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(h_j, e->a_pj.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  *h_len = n;
+}
+
+void align(wm_engine* e, int slot, int sot_len, const int* h_sot, int n_text, const int* h_text, int num_frames,
+           const int* h_heads, int n_heads, int medw, float* h_probs, int* h_ti, int* h_tj, int* h_len, hipStream_t st) {
+  const auto& m = e->dm;
+  const int T = m.n_audio_ctx, V = m.n_vocab;
+  const int S = sot_len + 1 + n_text + 1;
+  if (n_text <= 0 || S > m.n_text_ctx) throw std::runtime_error("wm_align: bad token count");
+  const int F = num_frames / 2;
+  if (F <= 0 || F > T) throw std::runtime_error("wm_align: bad num_frames");
+  std::vector<int> toks(S), next(n_text);
+  for (int i = 0; i < sot_len; ++i) toks[i] = h_sot[i];
+  toks[sot_len] = m.no_timestamps;
+  for (int i = 0; i < n_text; ++i) toks[sot_len + 1 + i] = next[i] = h_text[i];
+  toks[S - 1] = m.eot;
+  e->a_logits.ensure((size_t)S * V * 4);
+  e->a_attn.ensure((size_t)S * n_heads * T * 4);
+  forward(e, 1, &slot, S, toks.data(), e->a_logits.as<float>(), 0, h_heads, n_heads, e->a_attn.as<float>(), st);
+  // text token probabilities: position sot_len + k predicts text token k
+  e->a_next.ensure((size_t)n_text * 4);
+  e->a_probs.ensure((size_t)n_text * 4);
+  HIP_OK(hipMemcpyAsync(e->a_next.p, next.data(), n_text * 4, hipMemcpyHostToDevice, st));
+  launch_token_probs(e->a_logits.as<float>() + (size_t)sot_len * V, n_text, V, m.eot, e->a_next.as<int>(),
+                     e->a_probs.as<float>(), st);
+  // DTW input matrix rows sot_len .. S-2 (n_text + 1 rows)
+  const int nrows = n_text + 1;
+  e->a_rowsum.ensure((size_t)S * n_heads * 4);
+  e->a_z.ensure((size_t)n_heads * S * F * 4);
+  e->a_mat.ensure((size_t)nrows * F * 4);
+  launch_align_matrix(e->a_attn.as<float>(), S, n_heads, T, F, medw, sot_len, nrows, e->a_rowsum.as<float>(),
+                      e->a_z.as<float>(), e->a_mat.as<float>(), st);
+  HIP_OK(hipMemcpyAsync(h_probs, e->a_probs.p, n_text * 4, hipMemcpyDeviceToHost, st));
+  dtw_run(e, e->a_mat.as<float>(), nrows, F, h_ti, h_tj, h_len, st);
+}
+
 template <class F>
 int guarded(wm_engine* e, F&& f) {
   try {
@@ -874,6 +936,29 @@ int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_
 }
 
 int64_t wm_device_bytes(wm_engine* e) { return e ? (int64_t)e->device_bytes() : 0; }
+
+int wm_frame_energy(wm_engine* e, const float* d_pcm, int64_t n_samples, int32_t frame, float* d_db, void* stream) {
+  return guarded(e, [&] {
+    if (frame <= 0) throw std::runtime_error("wm_frame_energy: bad frame size");
+    const int frames = (int)((n_samples + frame - 1) / frame);
+    launch_frame_energy(d_pcm, n_samples, frame, frames, d_db, (hipStream_t)stream);
+  });
+}
+
+int wm_align(wm_engine* e, int32_t slot, int32_t sot_len, const int32_t* h_sot, int32_t n_text, const int32_t* h_text,
+             int32_t num_frames, const int32_t* h_heads, int32_t n_heads, int32_t median_filter_width, float* h_probs,
+             int32_t* h_text_idx, int32_t* h_time_idx, int32_t* h_path_len, void* stream) {
+  return guarded(e, [&] {
+    check_weights(e);
+    align(e, slot, sot_len, h_sot, n_text, h_text, num_frames, h_heads, n_heads, median_filter_width, h_probs, h_text_idx,
+          h_time_idx, h_path_len, (hipStream_t)stream);
+  });
+}
+
+int wm_dtw(wm_engine* e, const float* d_cost, int32_t n, int32_t m, int32_t* h_text_idx, int32_t* h_time_idx,
+           int32_t* h_path_len, void* stream) {
+  return guarded(e, [&] { dtw_run(e, d_cost, n, m, h_text_idx, h_time_idx, h_path_len, (hipStream_t)stream); });
+}
 
 int32_t wm_profile_classes(void) { return P_N; }
 const char* wm_profile_name(int32_t cls) { return (cls >= 0 && cls < P_N) ? kProfNames[cls] : ""; }

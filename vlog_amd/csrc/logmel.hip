@@ -129,3 +129,25 @@ void launch_ordered_to_float(const unsigned int* in, float* out, hipStream_t st)
   hipLaunchKernelGGL(ordered_to_float_kernel, dim3(1), dim3(1), 0, st, in, out);
   WM_LAUNCH_CHECK("ordered_to_float_kernel");
 }
+
+// Per-frame log energy for the VAD stand-in: db[i] = 10*log10(mean(x^2) + 1e-12) over samples [i*W, i*W+W)
+// (zero-padded tail), one wave per frame.
+__global__ void frame_energy_kernel(const float* __restrict__ pcm, long long n, int W, int frames, float* __restrict__ db) {
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= frames) return;
+  float s = 0.f;
+  for (int i = lane; i < W; i += 64) {
+    const long long k = (long long)f * W + i;
+    const float v = k < n ? pcm[k] : 0.f;
+    s = fmaf(v, v, s);
+  }
+  s = wave_sum(s);
+  if (lane == 0) db[f] = 10.0f * log10f(s / W + 1e-12f);
+}
+
+void launch_frame_energy(const float* pcm, long long n, int W, int frames, float* db, hipStream_t st) {
+  if (frames <= 0) return;
+  hipLaunchKernelGGL(frame_energy_kernel, dim3((frames + 3) / 4), dim3(256), 0, st, pcm, n, W, frames, db);
+  WM_LAUNCH_CHECK("frame_energy_kernel");
+}

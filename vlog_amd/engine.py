@@ -182,6 +182,15 @@ class GpuEngine:
         u = (u & 0x7FFFFFFF) if (u & 0x80000000) else (~u & 0xFFFFFFFF)
         return float(np.array([u], dtype=np.uint32).view(np.float32)[0])
 
+    def frame_energy_db(self, pcm: torch.Tensor, frame: int = 512) -> np.ndarray:
+        pcm = pcm.to(self.device, torch.float32).contiguous()
+        n = pcm.numel()
+        out = torch.empty(max(1, (n + frame - 1) // frame), device=self.device, dtype=torch.float32)
+        with torch.cuda.device(self.device):
+            _capi.check(self.lib.wm_frame_energy(self.h, C.c_void_p(pcm.data_ptr()), n, frame, C.c_void_p(out.data_ptr()),
+                                                 self.stream_ptr()), "wm_frame_energy")
+        return out.cpu().numpy()[: (n + frame - 1) // frame]
+
     def features(self, pcm: torch.Tensor) -> torch.Tensor:
         """faster-whisper FeatureExtractor(audio): clamped log-mel [n_mels, N//160 + 1] on device."""
         mel, gmax = self.logmel(pcm)
@@ -265,3 +274,35 @@ class GpuEngine:
                                             C.c_void_p(attn.data_ptr()) if attn is not None else None,
                                             self.stream_ptr()), "wm_forward")
         return logits, attn
+
+    def align(self, slot: int, sot_sequence: Sequence[int], text_tokens: Sequence[int], num_frames: int,
+              alignment_heads: Sequence[Tuple[int, int]], median_filter_width: int = 7):
+        """-> (text_token_probs [n_text], text_indices, time_indices) (CTranslate2 Whisper.align for one window)."""
+        sot = np.ascontiguousarray(sot_sequence, dtype=np.int32)
+        text = np.ascontiguousarray(text_tokens, dtype=np.int32)
+        heads = np.ascontiguousarray(np.asarray(alignment_heads, dtype=np.int32).reshape(-1, 2))
+        cap = len(text) + 1 + num_frames // 2 + 2
+        probs = np.zeros(max(len(text), 1), dtype=np.float32)
+        ti = np.zeros(cap, dtype=np.int32)
+        tj = np.zeros(cap, dtype=np.int32)
+        n = np.zeros(1, dtype=np.int32)
+        with torch.cuda.device(self.device):
+            _capi.check(self.lib.wm_align(self.h, slot, len(sot), _i32p(sot), len(text), _i32p(text), num_frames,
+                                          _i32p(heads), heads.shape[0], median_filter_width, _f32p(probs), _i32p(ti),
+                                          _i32p(tj), _i32p(n), self.stream_ptr()), "wm_align")
+        k = int(n[0])
+        return probs[: len(text)], ti[:k].copy(), tj[:k].copy()
+
+    def dtw(self, cost: torch.Tensor):
+        """DTW path of a device cost matrix [N, M] (f32)."""
+        cost = cost.to(self.device, torch.float32).contiguous()
+        N, M = cost.shape
+        ti = np.zeros(N + M + 2, dtype=np.int32)
+        tj = np.zeros(N + M + 2, dtype=np.int32)
+        n = np.zeros(1, dtype=np.int32)
+        with torch.cuda.device(self.device):
+            _capi.check(self.lib.wm_dtw(self.h, C.c_void_p(cost.data_ptr()), N, M, _i32p(ti), _i32p(tj), _i32p(n),
+                                        self.stream_ptr()), "wm_dtw")
+        k = int(n[0])
+        return ti[:k].copy(), tj[:k].copy()
+

@@ -180,7 +180,7 @@ class WhisperModel:
         self.engine = GpuEngine(self.dims, sd, self.device_index)
         del sd
         self.engine.reserve(1, 8)
-        self._lock = threading.Lock()
+        self._lock = threading.RLock()
         self.feature_size = self.dims.n_mels
         self.num_samples_per_token = HOP_LENGTH * INPUT_STRIDE
         self.frames_per_second = FRAMES_PER_SECOND
@@ -579,3 +579,234 @@ def merge_punctuations(alignment: List[dict], prepended: str, appended: str) -> 
         else:
             i = j
         j += 1
+
+
+@dataclass
+class WindowResult:
+    index: int
+    seek: int
+    size: int
+    time_offset: float
+    tokens: List[int]
+    avg_logprob: float
+    temperature: float
+    compression_ratio: float
+    no_speech_prob: float
+
+
+class BatchedInferencePipeline:
+    """Throughput mode (faster-whisper `BatchedInferencePipeline`): the file's 30 s windows — fixed, or bounded
+    by VAD speech chunks — are decoded independently (no previous-text prompt) in large batches on one GPU:
+    one encoder call per batch, cross-KV for every window resident in HBM, one on-device batched
+    greedy/beam decode, then a batched re-decode of the windows that need temperature fallback.
+    Window-sharding over several GPUs: vlog_amd/shard.py."""
+
+    def __init__(self, model: WhisperModel, max_batch_windows: int = 150):
+        self.model = model
+        self.max_batch_windows = max_batch_windows
+
+    # -- windows of the whole-file feature matrix
+    @staticmethod
+    def fixed_windows(content_frames: int) -> List[Tuple[int, int]]:
+        return [(s, min(N_FRAMES, content_frames - s)) for s in range(0, content_frames, N_FRAMES)]
+
+    @staticmethod
+    def vad_windows(chunks: List[dict], content_frames: int) -> List[Tuple[int, int]]:
+        """Merge speech chunks (sample ranges) greedily into windows of at most 30 s (frame ranges)."""
+        out: List[Tuple[int, int]] = []
+        cur_s = cur_e = None
+        for c in chunks:
+            s, e = c["start"] // HOP_LENGTH, min(content_frames, -(-c["end"] // HOP_LENGTH))
+            while e - s > N_FRAMES:                          # a single over-long chunk: cut in 30 s pieces
+                if cur_s is not None:
+                    out.append((cur_s, cur_e - cur_s)); cur_s = None
+                out.append((s, N_FRAMES)); s += N_FRAMES
+            if cur_s is None:
+                cur_s, cur_e = s, e
+            elif e - cur_s <= N_FRAMES:
+                cur_e = e
+            else:
+                out.append((cur_s, cur_e - cur_s)); cur_s, cur_e = s, e
+        if cur_s is not None and cur_e > cur_s:
+            out.append((cur_s, cur_e - cur_s))
+        return out
+
+    def decode_windows(self, features: torch.Tensor, windows: Sequence[Tuple[int, int]], time_offsets: Sequence[float],
+                       tokenizer: Tokenizer, options: TranscriptionOptions, seed: int = 0) -> List[WindowResult]:
+        m = self.model
+        eng = m.engine
+        st = m.dims.specials
+        prompt = list(tokenizer.sot_sequence) + ([tokenizer.no_timestamps] if options.without_timestamps else [])
+        if options.initial_prompt:
+            ip = (tokenizer.encode(" " + options.initial_prompt.strip()) if isinstance(options.initial_prompt, str)
+                  else list(options.initial_prompt))
+            prompt = [tokenizer.sot_prev] + ip[-(m.max_length // 2 - 1):] + prompt
+        max_length = min(m.max_length, len(prompt) + options.max_new_tokens) if options.max_new_tokens else m.max_length
+        mit = int(round(options.max_initial_timestamp / m.time_precision))
+        out: List[WindowResult] = []
+        B = self.max_batch_windows
+        per = max(options.beam_size, options.best_of, 1)
+        for b0 in range(0, len(windows), B):
+            wins = list(windows[b0: b0 + B])
+            with m._lock:
+                eng.reserve(len(wins), len(wins) * per)
+                enc = eng.encode(features, [w[0] for w in wins], [w[1] for w in wins])
+                eng.cross_kv(enc, 0)
+                del enc
+                pending = list(range(len(wins)))
+                results: dict = {}
+                tries: dict = {i: [] for i in pending}
+                for ti, T in enumerate(options.temperatures):
+                    if not pending:
+                        break
+                    sampling = T > 0
+                    res, _ = eng.generate(
+                        pending, [prompt] * len(pending), beam_size=1 if sampling else options.beam_size,
+                        patience=options.patience, length_penalty=options.length_penalty, max_length=max_length,
+                        temperature=T, num_hypotheses=options.best_of if sampling else 1, seed=seed + 7919 * ti + b0,
+                        suppress_tokens=options.suppress_tokens, suppress_blank=options.suppress_blank,
+                        max_initial_timestamp_index=mit, with_timestamps=not options.without_timestamps,
+                        sot_index=prompt.index(st.sot), check_every=8)
+                    still = []
+                    for i, r in zip(pending, res):
+                        alp = segs.avg_logprob(r.score, len(r.tokens), options.length_penalty)
+                        cr = segs.compression_ratio(tokenizer.decode(r.tokens).strip())
+                        fb, below = segs.needs_fallback(cr, alp, r.no_speech_prob, options.compression_ratio_threshold,
+                                                        options.log_prob_threshold, options.no_speech_threshold)
+                        tries[i].append((r, alp, T, cr, below))
+                        if fb:
+                            still.append(i)
+                        else:
+                            results[i] = (r, alp, T, cr)
+                    pending = still
+                for i in pending:                      # every temperature failed: best avg logprob
+                    cand = [t for t in tries[i] if t[4]] or tries[i]
+                    r, alp, _, cr, _ = max(cand, key=lambda t: t[1])
+                    results[i] = (r, alp, options.temperatures[-1], cr)
+            for i, (s, n) in enumerate(wins):
+                r, alp, T, cr = results[i]
+                out.append(WindowResult(b0 + i, s, n, time_offsets[b0 + i], r.tokens, alp, T, cr, r.no_speech_prob))
+        return out
+
+    def window_segments(self, wr: WindowResult, tokenizer: Tokenizer, options: TranscriptionOptions) -> List[dict]:
+        if segs.should_skip_window(wr.no_speech_prob, wr.avg_logprob, options.no_speech_threshold,
+                                   options.log_prob_threshold):
+            return []
+        dur = wr.size * HOP_LENGTH / SAMPLE_RATE
+        if options.without_timestamps:
+            cur = [dict(seek=wr.seek, start=wr.time_offset, end=wr.time_offset + dur,
+                        tokens=[t for t in wr.tokens if t < tokenizer.eot])]
+        else:
+            cur, _, _ = segs.split_segments_by_timestamps(wr.tokens, tokenizer.timestamp_begin, wr.time_offset,
+                                                          wr.size, dur, wr.seek)
+        return cur
+
+    def transcribe(self, audio: Union[str, BinaryIO, np.ndarray], language: Optional[str] = None,
+                   task: str = "transcribe", log_progress: bool = False, beam_size: int = 5, best_of: int = 5,
+                   patience: float = 1, length_penalty: float = 1, repetition_penalty: float = 1,
+                   no_repeat_ngram_size: int = 0,
+                   temperature: Union[float, List[float], Tuple[float, ...]] = (0.0, 0.2, 0.4, 0.6, 0.8, 1.0),
+                   compression_ratio_threshold: Optional[float] = 2.4, log_prob_threshold: Optional[float] = -1.0,
+                   no_speech_threshold: Optional[float] = 0.6, initial_prompt=None, prefix: Optional[str] = None,
+                   suppress_blank: bool = True, suppress_tokens: Optional[List[int]] = [-1],
+                   without_timestamps: bool = True, max_initial_timestamp: float = 1.0, word_timestamps: bool = False,
+                   prepend_punctuations: str = "\"'“¿([{-", append_punctuations: str = "\"'.。,，!！?？:：”)]}、",
+                   multilingual: bool = False, vad_filter: bool = True, vad_parameters=None,
+                   max_new_tokens: Optional[int] = None, chunk_length: Optional[int] = None, clip_timestamps=None,
+                   hallucination_silence_threshold: Optional[float] = None, batch_size: int = 16,
+                   hotwords: Optional[str] = None, language_detection_threshold: Optional[float] = 0.5,
+                   language_detection_segments: int = 1):
+        for name, val, default in (("repetition_penalty", repetition_penalty, 1), ("no_repeat_ngram_size", no_repeat_ngram_size, 0),
+                                   ("prefix", prefix, None), ("hotwords", hotwords, None), ("multilingual", multilingual, False),
+                                   ("hallucination_silence_threshold", hallucination_silence_threshold, None)):
+            if val != default:
+                raise NotImplementedError(f"{name}={val!r} is not supported by the MI355X engine")
+        m = self.model
+        if not isinstance(audio, np.ndarray):
+            audio = load_audio(audio)
+        audio = np.asarray(audio, dtype=np.float32)
+        duration = audio.shape[0] / SAMPLE_RATE
+        with m._lock:
+            features = m._features(audio)
+        content = features.shape[1] - 1
+        vad_opts = None
+        if vad_filter:
+            from .vad import get_speech_timestamps
+            vad_opts = vad_parameters if isinstance(vad_parameters, VadOptions) else VadOptions(**(vad_parameters or {}))
+            chunks = get_speech_timestamps(audio, vad_opts, m)
+            windows = self.vad_windows(chunks, content)
+            duration_after_vad = sum(c["end"] - c["start"] for c in chunks) / SAMPLE_RATE
+        else:
+            windows = self.fixed_windows(content)
+            duration_after_vad = duration
+        all_language_probs = None
+        if language is None:
+            if m.is_multilingual and windows:
+                language, language_probability, all_language_probs = m.detect_language(
+                    features=features, language_detection_segments=language_detection_segments,
+                    language_detection_threshold=language_detection_threshold or 0.5)
+            else:
+                language, language_probability = "en", 1.0
+        else:
+            language_probability = 1.0
+        tokenizer = m.tokenizer(task=task, language=language)
+        temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
+        options = TranscriptionOptions(
+            beam_size=beam_size, best_of=best_of, patience=patience, length_penalty=length_penalty,
+            repetition_penalty=repetition_penalty, no_repeat_ngram_size=no_repeat_ngram_size,
+            log_prob_threshold=log_prob_threshold, no_speech_threshold=no_speech_threshold,
+            compression_ratio_threshold=compression_ratio_threshold, condition_on_previous_text=False,
+            prompt_reset_on_temperature=0.5, temperatures=temps, initial_prompt=initial_prompt, prefix=prefix,
+            suppress_blank=suppress_blank,
+            suppress_tokens=list(tokenizer.suppressed_tokens(suppress_tokens)) if suppress_tokens else [],
+            without_timestamps=without_timestamps, max_initial_timestamp=max_initial_timestamp,
+            word_timestamps=word_timestamps, prepend_punctuations=prepend_punctuations,
+            append_punctuations=append_punctuations, multilingual=multilingual, max_new_tokens=max_new_tokens,
+            clip_timestamps=clip_timestamps or "0", hallucination_silence_threshold=hallucination_silence_threshold,
+            hotwords=hotwords)
+        offsets = [s * HOP_LENGTH / SAMPLE_RATE for s, _ in windows]
+        results = self.decode_windows(features, windows, offsets, tokenizer, options)
+        info = TranscriptionInfo(language=language, language_probability=language_probability, duration=duration,
+                                 duration_after_vad=duration_after_vad, all_language_probs=all_language_probs,
+                                 transcription_options=options, vad_options=vad_opts)
+        return self._segments(features, results, tokenizer, options), info
+
+    def _segments(self, features, results: List[WindowResult], tokenizer: Tokenizer, options: TranscriptionOptions):
+        m = self.model
+        idx = 0
+        last_speech = 0.0
+        for wr in results:
+            cur = self.window_segments(wr, tokenizer, options)
+            if options.word_timestamps and cur:
+                with m._lock:
+                    m._encode(features, wr.seek, wr.size, 0)
+                    last_speech = m.add_word_timestamps([cur], tokenizer, wr.size, options.prepend_punctuations,
+                                                        options.append_punctuations, last_speech)
+            for s in cur:
+                text = tokenizer.decode(s["tokens"])
+                if s["start"] == s["end"] or not text.strip():
+                    continue
+                idx += 1
+                yield Segment(id=idx, seek=wr.seek, start=s["start"], end=s["end"], text=text, tokens=s["tokens"],
+                              avg_logprob=wr.avg_logprob, compression_ratio=wr.compression_ratio,
+                              no_speech_prob=wr.no_speech_prob, temperature=wr.temperature,
+                              words=[Word(**w) for w in s["words"]] if options.word_timestamps else None)
+
+
+def default_batched_options(**kw) -> dict:
+    """TranscriptionOptions fields (as a dict) for the batched/sharded throughput mode."""
+    base = dict(beam_size=5, best_of=5, patience=1.0, length_penalty=1.0, repetition_penalty=1.0,
+                no_repeat_ngram_size=0, log_prob_threshold=-1.0, no_speech_threshold=0.6,
+                compression_ratio_threshold=2.4, condition_on_previous_text=False, prompt_reset_on_temperature=0.5,
+                temperatures=[0.0, 0.2, 0.4, 0.6, 0.8, 1.0], initial_prompt=None, prefix=None, suppress_blank=True,
+                suppress_tokens=[-1], without_timestamps=False, max_initial_timestamp=1.0, word_timestamps=False,
+                prepend_punctuations="\"'“¿([{-", append_punctuations="\"'.。,，!！?？:：”)]}、", multilingual=False,
+                max_new_tokens=None, clip_timestamps="0", hallucination_silence_threshold=None, hotwords=None)
+    if "temperature" in kw:
+        t = kw.pop("temperature")
+        kw["temperatures"] = list(t) if isinstance(t, (list, tuple)) else [t]
+    unknown = set(kw) - set(base)
+    if unknown:
+        raise TypeError(f"unknown options {sorted(unknown)}")
+    base.update(kw)
+    return base
