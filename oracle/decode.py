@@ -234,3 +234,23 @@ def detect_language(model, cross, st) -> List[tuple]:
     p = np.exp(log_softmax(lang))
     order = np.argsort(-p, kind="stable")
     return [(st.lang_codes[i], float(p[i])) for i in order]
+
+
+def score_sequence(model, cross, prompt: Sequence[int], tokens: Sequence[int], st, opt: GenerateOptions,
+                   ended_with_eot: bool = True):
+    """Teacher-force `tokens` (generated, no eot) through the oracle with the same rules.
+    -> (chosen_logprobs, best_logprobs, normalised_score): per step the rule-masked log-prob of the chosen
+    token (eot appended if `ended_with_eot`) and the best log-prob at that step, plus cum/len**lp."""
+    seq = list(tokens) + ([st.eot] if ended_with_eot else [])
+    toks = np.asarray([list(prompt) + list(tokens)])
+    logits, _ = model.decode(toks, cross)
+    P = len(prompt)
+    chosen, best = [], []
+    for i, t in enumerate(seq):
+        x = apply_rules(logits[0, P - 1 + i], list(tokens[:i]), st, opt.suppress_tokens, opt.suppress_blank,
+                        opt.max_initial_timestamp_index, opt.with_timestamps)
+        lp = log_softmax(x)
+        chosen.append(float(lp[t]))
+        best.append(float(np.max(lp)))
+    cum = float(np.sum(chosen))
+    return np.array(chosen), np.array(best), _norm(cum, len(tokens), opt.length_penalty)

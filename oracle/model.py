@@ -22,6 +22,15 @@ import numpy as np
 from scipy.special import erf
 
 
+def to_bf16(x: np.ndarray) -> np.ndarray:
+    """Round float32 values to bfloat16 (round-to-nearest-even) and return them as float32."""
+    x32 = np.ascontiguousarray(x, dtype=np.float32)
+    u = x32.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    out = r.astype(np.uint32).view(np.float32)
+    return np.where(np.isfinite(x32), out, x32).astype(np.float32)
+
+
 def gelu(x: np.ndarray) -> np.ndarray:
     return 0.5 * x * (1.0 + erf(x / np.sqrt(2.0)).astype(x.dtype))
 
@@ -58,14 +67,23 @@ def conv1d(x: np.ndarray, w: np.ndarray, b: np.ndarray, stride: int) -> np.ndarr
 
 
 class OracleWhisper:
-    def __init__(self, sd: Dict[str, np.ndarray], dims, dtype=np.float32):
+    """`bf16_acts=True` restates the engine's numeric format in the DECODER: activations are rounded to
+    bf16 exactly where libwhisper_mi355 stores them (LayerNorm outputs, q/k/v and the KV caches, attention
+    outputs, GELU outputs, cross K/V), with float32 accumulation everywhere else — so a token-identity test
+    compares the same arithmetic up to summation order instead of bf16 vs f32 rounding."""
+
+    def __init__(self, sd: Dict[str, np.ndarray], dims, dtype=np.float32, bf16_acts: bool = False):
         self.dims = dims
+        self.bf16 = bf16_acts
         self.dtype = dtype
         self.w = {k: np.asarray(v, dtype=dtype) for k, v in sd.items()}
         self.H = dims.n_head
         self.hd = dims.n_state // dims.n_head
 
     # ---------------------------------------------------------------- helpers
+    def _q(self, x):
+        return to_bf16(x) if self.bf16 else x
+
     def _lin(self, x, name, bias=True):
         y = x @ self.w[name + ".weight"].T
         if bias and (name + ".bias") in self.w:
@@ -114,7 +132,9 @@ class OracleWhisper:
         enc = np.asarray(enc, dtype=self.dtype)
         for i in range(self.dims.n_dec_layer):
             p = f"model.decoder.layers.{i}.encoder_attn."
-            out.append((self._split(self._lin(enc, p + "k_proj", bias=False)), self._split(self._lin(enc, p + "v_proj"))))
+            k = self._q(self._lin(self._q(enc), p + "k_proj", bias=False))
+            v = self._q(self._lin(self._q(enc), p + "v_proj"))
+            out.append((self._split(k), self._split(v)))
         return out
 
     def decode(self, tokens: np.ndarray, cross: List[Tuple[np.ndarray, np.ndarray]],
@@ -130,18 +150,18 @@ class OracleWhisper:
         cross_w = []
         for i in range(self.dims.n_dec_layer):
             p = f"model.decoder.layers.{i}."
-            h = layer_norm(x, w[p + "self_attn_layer_norm.weight"], w[p + "self_attn_layer_norm.bias"])
-            q = self._split(self._lin(h, p + "self_attn.q_proj"))
-            k = self._split(self._lin(h, p + "self_attn.k_proj", bias=False))
-            v = self._split(self._lin(h, p + "self_attn.v_proj"))
+            h = self._q(layer_norm(x, w[p + "self_attn_layer_norm.weight"], w[p + "self_attn_layer_norm.bias"]))
+            q = self._split(self._q(self._lin(h, p + "self_attn.q_proj")))
+            k = self._split(self._q(self._lin(h, p + "self_attn.k_proj", bias=False)))
+            v = self._split(self._q(self._lin(h, p + "self_attn.v_proj")))
             if cache is not None and offset > 0:
                 k = np.concatenate([cache[i][0], k], axis=2)
                 v = np.concatenate([cache[i][1], v], axis=2)
             new_cache.append((k, v))
             o, _ = self._attn(q, k, v, mask)
-            x = x + self._lin(self._merge(o), p + "self_attn.out_proj")
-            h = layer_norm(x, w[p + "encoder_attn_layer_norm.weight"], w[p + "encoder_attn_layer_norm.bias"])
-            q = self._split(self._lin(h, p + "encoder_attn.q_proj"))
+            x = x + self._lin(self._q(self._merge(o)), p + "self_attn.out_proj")
+            h = self._q(layer_norm(x, w[p + "encoder_attn_layer_norm.weight"], w[p + "encoder_attn_layer_norm.bias"]))
+            q = self._split(self._q(self._lin(h, p + "encoder_attn.q_proj")))
             ck, cv = cross[i]
             if ck.shape[0] != B:        # hypotheses sharing one window's cross-KV (beam search)
                 rep = B // ck.shape[0]
@@ -149,10 +169,10 @@ class OracleWhisper:
             o, pw = self._attn(q, ck, cv, return_weights=return_cross_attn)
             if return_cross_attn:
                 cross_w.append(pw)
-            x = x + self._lin(self._merge(o), p + "encoder_attn.out_proj")
-            h = layer_norm(x, w[p + "final_layer_norm.weight"], w[p + "final_layer_norm.bias"])
-            x = x + self._lin(gelu(self._lin(h, p + "fc1")), p + "fc2")
-        x = layer_norm(x, w["model.decoder.layer_norm.weight"], w["model.decoder.layer_norm.bias"])
+            x = x + self._lin(self._q(self._merge(o)), p + "encoder_attn.out_proj")
+            h = self._q(layer_norm(x, w[p + "final_layer_norm.weight"], w[p + "final_layer_norm.bias"]))
+            x = x + self._lin(self._q(gelu(self._lin(h, p + "fc1"))), p + "fc2")
+        x = self._q(layer_norm(x, w["model.decoder.layer_norm.weight"], w["model.decoder.layer_norm.bias"]))
         logits = x @ w["model.decoder.embed_tokens.weight"].T
         if return_cross_attn:
             return logits, new_cache, cross_w

@@ -48,17 +48,39 @@ def _split(tokens, tb, time_offset, segment_size, segment_duration, seek):
     return out, seek, single
 
 
+class OracleBackend:
+    """The oracle's own encoder + decoder for the loop below."""
+
+    def __init__(self, model, encoder=None):
+        self.model = model
+        self.encoder = encoder or (lambda w: model.encode(w[None]))
+
+    def encode(self, window):
+        return self.model.cross_kv(self.encoder(window))
+
+    def generate(self, cross, prompt, opt):
+        return generate_one(self.model, cross, prompt, self.model.dims.specials, opt)
+
+    def detect_language(self, cross):
+        return detect_language(self.model, cross, self.model.dims.specials)
+
+
 def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperatures=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0),
                condition_on_previous_text: bool = True, suppress_tokens: Optional[List[int]] = None,
-               word_timestamps: bool = False, language: Optional[str] = None):
-    """-> (segments [dict(start, end, text, tokens, avg_logprob, no_speech_prob, temperature, words)], language)."""
+               word_timestamps: bool = False, language: Optional[str] = None, encoder=None, features=None,
+               backend=None):
+    """`encoder(mel_window [n_mels, 3000]) -> [1, 1500, d]` overrides the oracle encoder so a test can compare
+    two decoders + host loops on the SAME encoder output (the encode/generate boundary); `features` likewise
+    overrides the log-mel (tested separately against oracle/mel.py); `backend` (encode / generate /
+    detect_language) replaces the oracle model entirely, so the HOST loops can be compared on one decoder.
+    -> (segments [dict(start, end, text, tokens, avg_logprob, no_speech_prob, temperature, words)], language)."""
     dims = model.dims
     st = dims.specials
-    feats = omel.log_mel(audio, dims.n_mels)
+    feats = omel.log_mel(audio, dims.n_mels) if features is None else np.asarray(features, dtype=np.float32)
     content = feats.shape[1] - 1
+    be = backend or OracleBackend(model, encoder)
     if language is None and dims.multilingual:
-        enc = model.encode(omel.pad_or_trim(feats[:, :3000])[None])
-        language = detect_language(model, model.cross_kv(enc), st)[0][0]
+        language = be.detect_language(be.encode(omel.pad_or_trim(feats[:, :3000])))[0][0]
     tok = tokenizer(language)
     sup = list(suppress_tokens) if suppress_tokens is not None else list(tok.suppressed_tokens([-1]))
     seek, all_tokens, reset_since, out = 0, [], 0, []
@@ -66,8 +88,7 @@ def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperat
         size = min(3000, content - seek)
         dur = size * 0.01
         toff = seek * 0.01
-        enc = model.encode(omel.pad_or_trim(feats[:, seek: seek + size])[None])
-        cross = model.cross_kv(enc)
+        cross = be.encode(omel.pad_or_trim(feats[:, seek: seek + size]))
         prev = all_tokens[reset_since:]
         prompt = ([st.sot_prev] + prev[-223:] if prev else []) + tok.sot_sequence
         results, below = [], []
@@ -76,7 +97,7 @@ def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperat
             opt = GenerateOptions(beam_size=beam_size if T == 0 else 1, patience=1.0, length_penalty=1.0, max_length=448,
                                   suppress_tokens=sup, suppress_blank=True, max_initial_timestamp_index=50,
                                   sampling_temperature=T, num_hypotheses=5 if T > 0 else 1, seed=i)
-            res = generate_one(model, cross, prompt, st, opt)
+            res = be.generate(cross, prompt, opt)
             n = len(res.tokens)
             alp = res.score * n / (n + 1)
             text = tok.decode(res.tokens).strip()

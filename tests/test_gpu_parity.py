@@ -25,6 +25,7 @@ def tiny():
     sd = synthetic_state_dict(dims, seed=3, eot_after=60)
     eng = GpuEngine(dims, sd, 0)
     orc = OracleWhisper(round_bf16(sd), dims, np.float32)
+    orc.bf = OracleWhisper(round_bf16(sd), dims, np.float32, bf16_acts=True)   # engine numeric format (decoder)
     return dims, eng, orc
 
 
@@ -80,6 +81,20 @@ def test_encoder_matches_oracle(tiny):
     assert err.mean() < 0.01, err.mean()
 
 
+def test_teacher_forced_logits_bf16_oracle(tiny):
+    """Against the oracle in the engine's numeric format the logits agree to summation-order noise."""
+    dims, eng, orc = tiny
+    st = dims.specials
+    feats = omel.log_mel(_audio(30.0, 22), dims.n_mels)
+    enc = eng.encode(torch.from_numpy(feats).cuda(), [0], [3000])
+    eng.reserve(4, 4)
+    eng.cross_kv(enc, 1)
+    toks = np.array([[st.sot, st.lang_token("en"), st.transcribe] + list(range(500, 540))])
+    logits, _ = eng.forward([1], toks)
+    ref, _ = orc.bf.decode(toks, orc.bf.cross_kv(enc.float().cpu().numpy()))
+    assert np.abs(logits.cpu().numpy() - ref).max() < 0.02
+
+
 def test_teacher_forced_logits(tiny):
     dims, eng, orc = tiny
     st = dims.specials
@@ -97,8 +112,14 @@ def test_teacher_forced_logits(tiny):
     assert np.abs(got - ref).max() < 0.02 * scale + 1e-3
 
 
+EPS = 0.02   # nats: the bf16 numeric noise floor of a logit (measured: ~0.006 max abs)
+
+
 def test_greedy_matches_oracle(tiny):
-    """Token identity at the generate boundary: both engines decode from the SAME encoder output."""
+    """Generate boundary, same encoder output.  Every GPU token, teacher-forced through the oracle with the
+    same rules, must be within EPS of the oracle's best log-prob at that step (exact identity is
+    ill-conditioned at near-ties of a random model); most windows are identical outright."""
+    from oracle.decode import score_sequence
     dims, eng, orc = tiny
     st = dims.specials
     W = 6
@@ -110,14 +131,17 @@ def test_greedy_matches_oracle(tiny):
     eng.cross_kv(enc, 0)
     prompt = [st.sot, st.lang_token("en"), st.transcribe]
     sup = [st.transcribe, st.translate, st.sot, st.sot_prev, st.sot_lm]
+    opt = GenerateOptions(suppress_tokens=sup, max_length=120)
     res, steps = eng.generate(list(range(W)), [prompt] * W, suppress_tokens=sup, max_length=120)
     encf = enc.float().cpu().numpy()
     same = 0
     for w in range(W):
         cross = orc.cross_kv(encf[w: w + 1])
-        r = generate_one(orc, cross, prompt, st, GenerateOptions(suppress_tokens=sup, max_length=120))
+        r = generate_one(orc, cross, prompt, st, opt)
         same += r.tokens == res[w].tokens
         assert abs(r.no_speech_prob - res[w].no_speech_prob) < 1e-3
-        if r.tokens == res[w].tokens:
-            assert abs(r.score - res[w].score) < 2e-2 * max(1.0, abs(r.score))
-    assert same / W >= 5 / 6, f"{same}/{W} windows identical"
+        ended = len(prompt) + len(res[w].tokens) < 120
+        chosen, best, score = score_sequence(orc, cross, prompt, res[w].tokens, st, opt, ended)
+        assert np.all(chosen >= best - EPS), np.min(chosen - best)
+        assert abs(score - res[w].score) < 2e-2 * max(1.0, abs(score))
+    assert same >= W - 1, f"{same}/{W} windows identical"

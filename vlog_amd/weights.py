@@ -135,9 +135,15 @@ def plant_eot(sd: Dict[str, torch.Tensor], dims: ModelDims, eot_after: int, seed
     sd["model.decoder.embed_tokens.weight"][dims.specials.eot] = c_e * u
 
 
+def stored_as_bf16(name: str, t: torch.Tensor) -> bool:
+    """Which tensors the engine keeps in bf16: weight matrices and conv kernels.  Biases, LayerNorm affines
+    and the position tables stay float32 (vlog_amd/engine.py pack_weights)."""
+    return name.endswith(".weight") and t.dim() >= 2 and "embed_positions" not in name
+
+
 def round_bf16(sd: Dict[str, torch.Tensor]) -> Dict[str, np.ndarray]:
-    """The values the GPU engine actually stores (bf16), as float32 numpy arrays for the oracle."""
-    return {k: v.to(torch.bfloat16).float().numpy() for k, v in sd.items()}
+    """The values the GPU engine actually stores, as float32 numpy arrays for the oracle."""
+    return {k: (v.to(torch.bfloat16).float() if stored_as_bf16(k, v) else v.float()).numpy() for k, v in sd.items()}
 
 
 # ----------------------------------------------------------------------------- local model directories
