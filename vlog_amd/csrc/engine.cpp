@@ -279,7 +279,7 @@ double gemm_bytes(double M, double N, double K, double out_bytes) { return 2 * M
 
 void gemm_p(wm_engine* e, int cls, const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& ep,
             hipStream_t st) {
-  const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_F32 || ep.kind == EPI_GELU_POS_F32) ? 4 : 2;
+  const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : (ep.kind == EPI_F32 || ep.kind == EPI_GELU_POS_F32) ? 4 : 2;
   ProfScope ps(e, cls, st, 2.0 * M * N * K, gemm_bytes(M, N, K, ob));
   // split-K only where the grid is too small to fill the chip (decoder rows); 64 MB slab scratch
   const size_t wsb = 64ull << 20;
@@ -406,15 +406,19 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
   {
     ProfScope ps(e, P_DEC_OTHER, st);
     launch_embed(row_tok, row_pos, e->Wb("dec.embed"), e->Wf("dec.pos"), x, rows, d, st);
+    launch_layernorm(x, d, nullptr, rows, d, e->Wf("dec.0.ln1.w"), e->Wf("dec.0.ln1.b"), hb, d, st);
   }
+  // residual-producing GEMMs also apply the LayerNorm that consumes the residual (EPI_RESID_LN: fused into
+  // the split-K combine on the skinny path): out -> ln2, cout -> ln3, fc2 -> next layer's ln1
+  auto resid_ln = [&](const std::string& ln) {
+    GemmEpi ep = epi_of(EPI_RESID_LN, x, d, nullptr);
+    ep.ln_g = e->Wf(ln + ".w"); ep.ln_b = e->Wf(ln + ".b"); ep.ln_out = hb; ep.ln_ld = d;
+    return ep;
+  };
   for (int l = 0; l < L; ++l) {
     const std::string p = "dec." + std::to_string(l) + ".";
     bf16* kc = skv + (size_t)(2 * l) * skv_layer;
     bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
-    {
-      ProfScope ps(e, P_DEC_OTHER, st);
-      launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln1.w"), e->Wf(p + "ln1.b"), hb, d, st);
-    }
     {
       GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, e->Wf(p + "qkv.b"));
       ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
@@ -425,10 +429,10 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
       ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
       launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
     }
-    gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "out.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "out.b")), st);
     {
-      ProfScope ps(e, P_DEC_OTHER, st);
-      launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln2.w"), e->Wf(p + "ln2.b"), hb, d, st);
+      GemmEpi ep = resid_ln(p + "ln2");
+      ep.bias = e->Wf(p + "out.b");
+      gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "out.w"), d, rows, d, d, ep, st);
     }
     gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "cq.w"), d, rows, d, d, epi_of(EPI_BF16, q, d, e->Wf(p + "cq.b")), st);
     float* probs = nullptr;
@@ -451,17 +455,23 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
                         splits == 1 ? ps.a : nullptr, splits == 1 ? ps.b : nullptr);
     }
     if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
-    gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "cout.w"), d, rows, d, d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "cout.b")), st);
     {
-      ProfScope ps(e, P_DEC_OTHER, st);
-      launch_layernorm(x, d, nullptr, rows, d, e->Wf(p + "ln3.w"), e->Wf(p + "ln3.b"), hb, d, st);
+      GemmEpi ep = resid_ln(p + "ln3");
+      ep.bias = e->Wf(p + "cout.b");
+      gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "cout.w"), d, rows, d, d, ep, st);
     }
     {
       GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, e->Wf(p + "fc1.b"));
       ep.act = 1;
       gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "fc1.w"), d, rows, 4 * d, d, ep, st);
     }
-    gemm_p(e, P_DEC_GEMM, amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
+    if (l + 1 < L) {
+      GemmEpi ep = resid_ln("dec." + std::to_string(l + 1) + ".ln1");
+      ep.bias = e->Wf(p + "fc2.b");
+      gemm_p(e, P_DEC_GEMM, amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, ep, st);
+    } else {
+      gemm_p(e, P_DEC_GEMM, amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
+    }
   }
   {
     ProfScope ps(e, P_DEC_OTHER, st);

@@ -17,6 +17,7 @@ enum EpiKind {
   EPI_F32 = 3,         // C_f32[r,c]  = acc (+ bias)
   EPI_DEC_QKV = 4,     // decoder self-attn: q -> C_bf16, k/v -> self-KV cache at (row_hyp[r], row_pos[r])
   EPI_CROSS_KV = 5,    // cross-KV projection -> [L][2][slots][H][T][hd]
+  EPI_RESID_LN = 6,    // X_f32[r,c] += acc + bias[c], then ln_out[r] = LayerNorm(X[r]) (bf16) — N == row width
 };
 
 struct GemmEpi {
@@ -35,8 +36,14 @@ struct GemmEpi {
   int d, n_head, head_dim, n_ctx;
   // EPI_CROSS_KV
   int n_slots, slot0;
+  // EPI_RESID_LN: the LayerNorm that consumes the updated residual
+  const float* ln_g; const float* ln_b; bf16* ln_out; long long ln_ld;
 };
 
 // ws: f32 scratch for split-K partial slabs (nullptr disables split-K)
 void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                  size_t ws_bytes, hipStream_t st);
+
+// Large-M path (gemm_big.hip): 256x128 tiles, LDS-DMA ring; used by launch_gemm when applicable.
+bool gemm_big_applicable(int M, int N, int K);
+void launch_gemm_big(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st);

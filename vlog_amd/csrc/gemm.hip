@@ -10,65 +10,17 @@
 // ds_read_b128 lane groups hit 16 distinct bank slots.  Grid is XCD-remapped (T1) so consecutive N-tiles
 // of one M-panel share an XCD's L2.
 #include "gemm.h"
+#include "gemm_epi.h"
+#include <cstdlib>
 #include <algorithm>
 #include <stdexcept>
 #include <string>
 
 #define BK 64
 
-__device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ ((row >> 1) & 7)) << 3); }
+void launch_layernorm(const float*, long long, const int*, int, int, const float*, const float*, bf16*, long long, hipStream_t);
 
-template <int KIND>
-__device__ __forceinline__ void apply_epi(const GemmEpi& epi, int row, int col, float acc) {
-  float v = acc + (epi.bias ? epi.bias[col] : 0.f);
-  switch (KIND) {
-    case EPI_BF16: {
-      if (epi.act == 1) v = gelu_erf(v);
-      long long o = epi.rpb ? (long long)(row / epi.rpb) * epi.bstride + (long long)(row % epi.rpb + epi.roff) * epi.ldc
-                            : (long long)row * epi.ldc;
-      ((bf16*)epi.out)[o + col] = f2bf(v);
-      break;
-    }
-    case EPI_RESID_F32: {
-      float* p = (float*)epi.out + (long long)row * epi.ldc + col;
-      *p += v;
-      break;
-    }
-    case EPI_GELU_POS_F32: {
-      const int t = row % epi.rpb;
-      ((float*)epi.out)[(long long)row * epi.ldc + col] = gelu_erf(v) + epi.pos[(long long)t * epi.ldc + col];
-      break;
-    }
-    case EPI_F32: {
-      ((float*)epi.out)[(long long)row * epi.ldc + col] = v;
-      break;
-    }
-    case EPI_DEC_QKV: {
-      const int d = epi.d;
-      if (col < d) {
-        ((bf16*)epi.out)[(long long)row * epi.ldc + col] = f2bf(v);
-      } else {
-        const int c2 = col - d;
-        const int kv = c2 >= d;
-        const int cc = kv ? c2 - d : c2;
-        const int h = cc / epi.head_dim, e2 = cc - h * epi.head_dim;
-        const long long slot = (((long long)epi.row_hyp[row] * epi.n_head + h) * epi.n_ctx + epi.row_pos[row]) * epi.head_dim + e2;
-        (kv ? epi.vcache : epi.kcache)[slot] = f2bf(v);
-      }
-      break;
-    }
-    case EPI_CROSS_KV: {
-      // col = l*2d + kv*d + h*hd + e ; row = b*T + t  ->  [L*2][slots][H][T][hd]
-      const int d = epi.d, hd = epi.head_dim;
-      const int l2 = col / d, cc = col - l2 * d;
-      const int h = cc / hd, e2 = cc - h * hd;
-      const int b = row / epi.rpb, t = row - b * epi.rpb;
-      const long long o = ((((long long)l2 * epi.n_slots + epi.slot0 + b) * epi.n_head + h) * epi.rpb + t) * hd + e2;
-      ((bf16*)epi.out)[o] = f2bf(v);
-      break;
-    }
-  }
-}
+__device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ ((row >> 1) & 7)) << 3); }
 
 template <int BM, int BN, int WM, int WN, int KIND>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmA a, const bf16* __restrict__ w, long long ldw,
@@ -193,10 +145,240 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const long long total = (long long)M * N;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     float v = 0.f;
+#pragma unroll 4
     for (int s = 0; s < splitk; ++s) v += part[s * total + i];
     const int row = (int)(i / N), col = (int)(i - (long long)row * N);
     apply_epi<KIND>(epi, row, col, v);
   }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Skinny path (decoder rows, M <= 256): the weight stream is the whole cost, so nothing about W touches LDS.
+// A block = 4 waves x 16 output columns (64 columns) over a K range [kb, kb + kr); each wave loads its
+// B fragments (W rows n, 16 B at k = 32kk + 8(lane>>4)) for a whole KS chunk straight into registers —
+// all KS/32 loads issued back to back, so every CU keeps its share of W in flight at once — while the
+// block's A rows [0, 16 MF) x chunk are DMA'd into LDS (global_load_lds, 128-B panel rows, XOR swizzle on
+// the source address) and shared by the 4 waves.  K is split across blocks until the grid covers the chip;
+// partial slabs are combined in split order by the reduce kernels below (deterministic).
+template <int MF, int KS, int KIND>
+__global__ __launch_bounds__(256) void skinny_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
+                                                     int K, GemmEpi epi, int tiles_n, int splitk, int kr,
+                                                     float* __restrict__ part) {
+  constexpr int ROWS = MF * 16, PANEL = ROWS * 64, NF = KS / 32;
+  __shared__ __attribute__((aligned(16))) bf16 sA[(KS / 64) * PANEL];
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int split = wgid % splitk, tile = wgid / splitk;
+  const int n0 = tile * 64;
+  const int kb = split * kr, kend = min(K, kb + kr);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ncol = n0 + wid * 16 + (lane & 15);
+  const bf16* wrow = w + (long long)min(ncol, N - 1) * ldw + 8 * (lane >> 4);
+
+  f32x4 acc[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c0 = kb; c0 < kend; c0 += KS) {
+    const int clen = min(KS, kend - c0);
+    bf16x8 fb[NF];
+#pragma unroll
+    for (int kk = 0; kk < NF; ++kk) fb[kk] = *(const bf16x8*)(wrow + c0 + min(32 * kk, clen - 32));
+    const int ngrp = (clen / 64) * (2 * MF);
+    for (int g = wid; g < ngrp; g += 4) {
+      const int panel = g / (2 * MF), rg = g - panel * (2 * MF);
+      const int row = rg * 8 + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
+      const int gr = min(row, M - 1);
+      const long long off = a.rpb ? (long long)(gr / a.rpb) * a.bstride + (long long)(gr % a.rpb) * a.ld : (long long)gr * a.ld;
+      __builtin_amdgcn_global_load_lds((const void*)(a.ptr + off + c0 + panel * 64 + ch * 8),
+                                       (__attribute__((address_space(3))) void*)(sA + panel * PANEL + rg * 8 * 64), 16, 0, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < NF; ++kk) {
+      if (32 * kk < clen) {
+        const int ch = (kk & 1) * 4 + (lane >> 4);
+        const bf16* pa = sA + (kk >> 1) * PANEL;
+        bf16x8 fa[MF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i) fa[i] = *(const bf16x8*)(pa + swz(i * 16 + (lane & 15), ch));
+#pragma unroll
+        for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[kk], acc[i], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, MF, 0);   // all MF ds_reads of this k-step first,
+        __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);   // then the MF MFMAs
+      }
+    }
+    __syncthreads();
+  }
+
+  if (ncol >= N) return;
+  const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = i * 16 + (lane >> 4) * 4 + e;
+      if (row >= M) continue;
+      if (to_slab)
+        part[((long long)split * M + row) * N + ncol] = acc[i][e];
+      else
+        apply_epi<KIND>(epi, row, ncol, acc[i][e]);
+    }
+  }
+}
+
+// Split-K combine fused with the residual add and the LayerNorm that consumes it: one 256-thread block per
+// row, thread t owns float2 pairs t, t+256, ... (J = ceil(N/512)); the slab loop is unrolled 4-deep so 4*J
+// loads are in flight per thread.  x[r] += sum_s part[s][r] + bias;  ln_out[r] = LN(x[r]) (two-pass
+// mean / variance over the block, eps 1e-5).  Summation order per element = splitk_reduce_kernel's.
+template <int J>
+__global__ __launch_bounds__(256) void resid_ln_reduce_kernel(const float* __restrict__ part, int splitk, int M, int N,
+                                                              GemmEpi epi) {
+  __shared__ float red[2][4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int np = N >> 1;
+  const long long slab = (long long)M * N;
+  const float2* pr = (const float2*)(part + (long long)r * N);
+  float2 acc[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) acc[j] = make_float2(0.f, 0.f);
+#pragma unroll 4
+  for (int sp = 0; sp < splitk; ++sp) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int c = tid + 256 * j;
+      if (c < np) {
+        const float2 v = pr[(sp * slab >> 1) + c];
+        acc[j].x += v.x;
+        acc[j].y += v.y;
+      }
+    }
+  }
+  float2* xr = (float2*)((float*)epi.out + (long long)r * epi.ldc);
+  const float2* b2 = (const float2*)epi.bias;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c = tid + 256 * j;
+    if (c < np) {
+      float2 v = acc[j];
+      if (b2) {
+        const float2 bb = b2[c];
+        v.x += bb.x;
+        v.y += bb.y;
+      }
+      float2 xv = xr[c];
+      xv.x += v.x;
+      xv.y += v.y;
+      xr[c] = xv;
+      acc[j] = xv;
+      s += xv.x + xv.y;
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[0][wid] = s;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)N;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c = tid + 256 * j;
+    if (c < np) {
+      const float a = acc[j].x - mean, b = acc[j].y - mean;
+      q += a * a + b * b;
+    }
+  }
+  q = wave_sum(q);
+  if (lane == 0) red[1][wid] = q;
+  __syncthreads();
+  const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)N + 1e-5f);
+  bf16x2* yr = (bf16x2*)(epi.ln_out + (long long)r * epi.ln_ld);
+  const float2* g2 = (const float2*)epi.ln_g;
+  const float2* lb2 = (const float2*)epi.ln_b;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c = tid + 256 * j;
+    if (c < np) {
+      const float2 gg = g2[c], bb = lb2[c];
+      bf16x2 o;
+      o[0] = f2bf((acc[j].x - mean) * rstd * gg.x + bb.x);
+      o[1] = f2bf((acc[j].y - mean) * rstd * gg.y + bb.y);
+      yr[c] = o;
+    }
+  }
+}
+
+static void launch_resid_ln_reduce(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st) {
+  if (N % 2 != 0 || N > 2048) throw std::runtime_error("resid_ln_reduce: unsupported width " + std::to_string(N));
+  dim3 grid(M), block(256);
+  if (N <= 512) hipLaunchKernelGGL(resid_ln_reduce_kernel<1>, grid, block, 0, st, part, splitk, M, N, epi);
+  else if (N <= 1024) hipLaunchKernelGGL(resid_ln_reduce_kernel<2>, grid, block, 0, st, part, splitk, M, N, epi);
+  else if (N <= 1536) hipLaunchKernelGGL(resid_ln_reduce_kernel<3>, grid, block, 0, st, part, splitk, M, N, epi);
+  else hipLaunchKernelGGL(resid_ln_reduce_kernel<4>, grid, block, 0, st, part, splitk, M, N, epi);
+  WM_LAUNCH_CHECK("resid_ln_reduce_kernel");
+}
+
+// Skinny-path geometry: split K so the grid reaches ~256 blocks, each split at least 128 deep (partial
+// slabs cost 8 B per output per split); returns false when the slabs do not fit the scratch.
+static bool skinny_plan(int M, int N, int K, size_t ws_bytes, int* splitk, int* kr) {
+  const int tiles_n = (N + 63) / 64;
+  int s = std::max(1, (256 + tiles_n / 2) / tiles_n);
+  s = std::min(s, std::max(1, K / 128));
+  int k = ((K + s - 1) / s + 63) / 64 * 64;
+  s = (K + k - 1) / k;
+  while (s > 1 && (size_t)s * M * N * 4 > ws_bytes) {
+    --s;
+    k = ((K + s - 1) / s + 63) / 64 * 64;
+    s = (K + k - 1) / k;
+  }
+  *splitk = s;
+  *kr = k;
+  return (size_t)s * M * N * 4 <= ws_bytes;
+}
+
+template <int MF, int KS, int KIND>
+static void run_skinny(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                       int splitk, int kr, hipStream_t st) {
+  const int tiles_n = (N + 63) / 64;
+  hipLaunchKernelGGL((skinny_kernel<MF, KS, KIND>), dim3(tiles_n * splitk), dim3(256), 0, st, a, w, ldw, M, N, K, epi,
+                     tiles_n, splitk, kr, ws);
+  WM_LAUNCH_CHECK("skinny_kernel");
+  if (KIND == EPI_RESID_LN) {
+    launch_resid_ln_reduce(ws, splitk, M, N, epi, st);
+  } else if (splitk > 1) {
+    const long long total = (long long)M * N;
+    int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL((splitk_reduce_kernel<KIND>), dim3(blocks), dim3(256), 0, st, ws, splitk, M, N, epi);
+    WM_LAUNCH_CHECK("splitk_reduce_kernel");
+  }
+}
+
+template <int KIND>
+static void dispatch_skinny(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
+                            float* ws, int splitk, int kr, hipStream_t st) {
+  if (M <= 16) run_skinny<1, 512, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 32) run_skinny<2, 512, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 64) run_skinny<4, 512, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 128) run_skinny<8, 256, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 160) run_skinny<10, 256, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_skinny<16, 128, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+}
+
+static bool try_skinny(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                       size_t ws_bytes, hipStream_t st) {
+  if (M > 256 || !ws) return false;
+  int splitk, kr;
+  if (!skinny_plan(M, N, K, ws_bytes, &splitk, &kr)) return false;
+  switch (epi.kind) {
+    case EPI_BF16: dispatch_skinny<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_RESID_F32: dispatch_skinny<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_F32: dispatch_skinny<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_DEC_QKV: dispatch_skinny<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_RESID_LN: dispatch_skinny<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    default: return false;
+  }
+  return true;
 }
 
 template <int BM, int BN, int WM, int WN, int KIND>
@@ -246,6 +428,26 @@ void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int
                  size_t ws_bytes, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   if (K % BK != 0) throw std::runtime_error("launch_gemm: K must be a multiple of 64 (got " + std::to_string(K) + ")");
+  static const bool big_enabled = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_BIG");
+    return !(e && e[0] == '0');
+  }();
+  static const bool skinny_enabled = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_SKINNY");
+    return !(e && e[0] == '0');
+  }();
+  if (skinny_enabled && try_skinny(a, w, ldw, M, N, K, epi, ws, ws_bytes, st)) return;
+  if (epi.kind == EPI_RESID_LN) {        // unfused form: residual epilogue, then the LayerNorm
+    GemmEpi r = epi;
+    r.kind = EPI_RESID_F32;
+    launch_gemm(a, w, ldw, M, N, K, r, ws, ws_bytes, st);
+    launch_layernorm((const float*)epi.out, epi.ldc, nullptr, M, N, epi.ln_g, epi.ln_b, epi.ln_out, epi.ln_ld, st);
+    return;
+  }
+  if (big_enabled && gemm_big_applicable(M, N, K)) {
+    launch_gemm_big(a, w, ldw, M, N, K, epi, st);
+    return;
+  }
   switch (epi.kind) {
     case EPI_BF16: dispatch<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, ws_bytes, st); break;
     case EPI_RESID_F32: dispatch<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, ws_bytes, st); break;
