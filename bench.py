@@ -177,17 +177,26 @@ def main():
 
     for _ in range(args.warmup):
         pipe.step()
+    # one untimed step with every kernel class under events: the per-class breakdown and the dominant class
+    breakdown, dom = None, None
+    if not args.no_profile:
+        barrier()
+        eng.profile(True)
+        pipe.step()
+        eng.profile(False)
+        breakdown = eng.profile_read()
+        dom = max(breakdown, key=lambda k: breakdown[k]["ms"])
     pipe.stage = {}
     barrier()
-    if not args.no_profile:
-        eng.profile(True)
+    if dom is not None:                       # timed region: events on the dominant class only
+        eng.profile(True, classes=[dom])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pipe.step()
     barrier()
     elapsed = time.perf_counter() - t0
     prof = None
-    if not args.no_profile:
+    if dom is not None:
         eng.profile(False)
         prof = eng.profile_read()
     if world > 1:
@@ -217,15 +226,14 @@ def main():
     }
     if prof:
         kern = {}
-        for k, v in prof.items():
+        for k, v in breakdown.items():
             if v["launches"] == 0:
                 continue
             kern[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
                        "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["flops"] else None,
                        "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["bytes"] else None}
-        out["kernels"] = kern
-        dom = max(kern, key=lambda k: kern[k]["ms"])
-        v = prof[dom]
+        out["kernels_one_step"] = kern
+        v = prof[dom]                          # measured over the timed region
         if dom in ("cross_attn", "self_attn", "select", "dec_other", "logmel") or (v["flops"] == 0):
             ach = v["bytes"] / (v["ms"] * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -235,6 +243,8 @@ def main():
             roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
                     "frac": round(ach / MFMA_BF16_PEAK_TFS, 4)}
         roof["kernel"] = dom
+        roof["launches"] = v["launches"]
+        roof["avg_launch_us"] = round(1000.0 * v["ms"] / max(v["launches"], 1), 2)
         roof["traffic"] = None
         if os.path.isfile(args.traffic_json):
             try:
@@ -242,12 +252,12 @@ def main():
                 roof["traffic"] = tj.get(dom)
             except Exception:
                 pass
-        enc_ms = sum(prof[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
-        enc_fl = sum(prof[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
         out["roofline"] = roof
+        enc_ms = sum(breakdown[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
+        enc_fl = sum(breakdown[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
         out["encoder_mfma"] = {"achieved_tflops": round(enc_fl / max(enc_ms, 1e-9) / 1e9, 1),
                                "frac_of_2500": round(enc_fl / max(enc_ms, 1e-9) / 1e9 / MFMA_BF16_PEAK_TFS, 4)}
-        cx = prof["cross_attn"]
+        cx = breakdown["cross_attn"]
         out["decoder_kv_read"] = {"achieved_gbs": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6, 1),
                                   "frac_of_8000": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6 / HBM_PEAK_GBS, 4)}
     if world == 1 and not args.no_cpu_baseline and sd is not None:

@@ -135,6 +135,9 @@ int64_t wm_device_bytes(wm_engine* e);
 int32_t wm_profile_classes(void);
 const char* wm_profile_name(int32_t cls);
 int wm_profile(wm_engine* e, int32_t enable);
+/* As wm_profile(e, 1) but only the classes whose bit is set in class_mask are timed (0 disables), so a
+ * timed run can keep events on the dominant kernel alone. */
+int wm_profile_select(wm_engine* e, uint32_t class_mask);
 int wm_profile_read(wm_engine* e, int32_t cls, int64_t* launches, double* ms, double* flops, double* bytes);
 
 #ifdef __cplusplus

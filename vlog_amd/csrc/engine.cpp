@@ -112,6 +112,7 @@ struct wm_engine {
   DevBuf s_x, s_hb, s_q, s_ao, s_ff, s_logits, s_pm, s_pl, s_po;
   // profiler: per class, HIP event pairs recorded on the launch stream + algorithmic flops / bytes
   bool prof_on = false;
+  unsigned prof_mask = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[P_N];
   std::vector<hipEvent_t> ev_pool;
   double prof_flops[P_N] = {0}, prof_bytes[P_N] = {0};
@@ -128,7 +129,7 @@ struct wm_engine {
     ev_pool.pop_back();
     return ev;
   }
-  unsigned long long* dstat(int cls) { return prof_on ? prof_dbytes.as<unsigned long long>() + cls : nullptr; }
+  unsigned long long* dstat(int cls) { return (prof_on && ((prof_mask >> cls) & 1u)) ? prof_dbytes.as<unsigned long long>() + cls : nullptr; }
 
   const Slot& slot(const std::string& n) const {
     auto it = slots.find(n);
@@ -260,7 +261,7 @@ struct ProfScope {
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(wm_engine* e_, int cls_, hipStream_t st_, double flops = 0, double bytes = 0, bool attached_ = false)
       : e(e_), cls(cls_), st(st_), attached(attached_) {
-    if (!e->prof_on) return;
+    if (!e->prof_on || !((e->prof_mask >> cls) & 1u)) return;
     a = e->ev_get();
     b = e->ev_get();
     if (!attached) HIP_OK(hipEventRecord(a, st));
@@ -973,10 +974,10 @@ int wm_dtw(wm_engine* e, const float* d_cost, int32_t n, int32_t m, int32_t* h_t
 int32_t wm_profile_classes(void) { return P_N; }
 const char* wm_profile_name(int32_t cls) { return (cls >= 0 && cls < P_N) ? kProfNames[cls] : ""; }
 
-int wm_profile(wm_engine* e, int32_t enable) {
+int wm_profile_select(wm_engine* e, uint32_t class_mask) {
   return guarded(e, [&] {
     HIP_OK(hipDeviceSynchronize());
-    if (!enable) {            // stop recording; keep what was recorded for wm_profile_read
+    if (!class_mask) {        // stop recording; keep what was recorded for wm_profile_read
       e->prof_on = false;
       return;
     }
@@ -988,9 +989,12 @@ int wm_profile(wm_engine* e, int32_t enable) {
     }
     e->prof_dbytes.ensure(P_N * sizeof(unsigned long long));
     HIP_OK(hipMemset(e->prof_dbytes.p, 0, P_N * sizeof(unsigned long long)));
+    e->prof_mask = class_mask;
     e->prof_on = true;
   });
 }
+
+int wm_profile(wm_engine* e, int32_t enable) { return wm_profile_select(e, enable ? ((1u << P_N) - 1u) : 0u); }
 
 int wm_profile_read(wm_engine* e, int32_t cls, int64_t* launches, double* ms, double* flops, double* bytes) {
   return guarded(e, [&] {

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmA a, const bf16* __rest
 #pragma unroll
         for (int i = 0; i < MF; ++i) fa[i] = *(const bf16x8*)(pa + swz(i * 16 + (lane & 15), ch));
 #pragma unroll
-        for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[kk], acc[i], 0, 0, 0);
+        for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk], fa[i], acc[i], 0, 0, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, MF, 0);   // all MF ds_reads of this k-step first,
         __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);   // then the MF MFMAs
       }
@@ -212,110 +212,98 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmA a, const bf16* __rest
     __syncthreads();
   }
 
-  if (ncol >= N) return;
+  // operands are swapped (W fragment as the MFMA A operand): acc[i] holds C^T, lane l has row
+  // m = 16 i + (l & 15) and the 4 consecutive columns n = col0 + e -> one 16-B slab store per fragment
   const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
+  const int col0 = n0 + wid * 16 + 4 * (lane >> 4);
+  const bool vec = (N % 4 == 0) && (to_slab || (epi.ldc % 4 == 0 && (epi.rpb == 0 || epi.bstride % 4 == 0)));
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = i * 16 + (lane >> 4) * 4 + e;
-      if (row >= M) continue;
+    const int row = i * 16 + (lane & 15);
+    if (row >= M) continue;
+    if (vec && col0 < N) {
       if (to_slab)
-        part[((long long)split * M + row) * N + ncol] = acc[i][e];
+        *(f32x4*)(part + ((long long)split * M + row) * N + col0) = acc[i];
       else
-        apply_epi<KIND>(epi, row, ncol, acc[i][e]);
+        apply_epi4<KIND>(epi, row, col0, acc[i]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (col0 + e >= N) continue;
+        if (to_slab)
+          part[((long long)split * M + row) * N + col0 + e] = acc[i][e];
+        else
+          apply_epi<KIND>(epi, row, col0 + e, acc[i][e]);
+      }
     }
   }
 }
 
-// Split-K combine fused with the residual add and the LayerNorm that consumes it: one 256-thread block per
-// row, thread t owns float2 pairs t, t+256, ... (J = ceil(N/512)); the slab loop is unrolled 4-deep so 4*J
-// loads are in flight per thread.  x[r] += sum_s part[s][r] + bias;  ln_out[r] = LN(x[r]) (two-pass
-// mean / variance over the block, eps 1e-5).  Summation order per element = splitk_reduce_kernel's.
-template <int J>
-__global__ __launch_bounds__(256) void resid_ln_reduce_kernel(const float* __restrict__ part, int splitk, int M, int N,
-                                                              GemmEpi epi) {
-  __shared__ float red[2][4];
-  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+// Split-K combine fused with the residual add and the LayerNorm that consumes it: one block per row, one
+// thread per float2 pair (N/2 threads, up to 16 waves), the slab loop unrolled 8-deep so a thread has 8
+// loads in flight (150 decoder rows cannot fill the chip, so latency, not bandwidth, is the cost).
+// x[r] += sum_s part[s][r] + bias;  ln_out[r] = LN(x[r]) (two-pass mean / variance, eps 1e-5).  Summation
+// order per element = splitk_reduce_kernel's.
+__global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __restrict__ part, int splitk, int M, int N,
+                                                               GemmEpi epi) {
+  __shared__ float red[2][16];
+  const int r = blockIdx.x, c = threadIdx.x, lane = c & 63, wid = c >> 6, nw = blockDim.x >> 6;
   const int np = N >> 1;
-  const long long slab = (long long)M * N;
-  const float2* pr = (const float2*)(part + (long long)r * N);
-  float2 acc[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) acc[j] = make_float2(0.f, 0.f);
-#pragma unroll 4
+  const bool act = c < np;
+  const long long slab2 = ((long long)M * N) >> 1;
+  const float2* pr = (const float2*)(part + (long long)r * N) + (act ? c : 0);
+  float2 acc = make_float2(0.f, 0.f);
+#pragma unroll 8
   for (int sp = 0; sp < splitk; ++sp) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int c = tid + 256 * j;
-      if (c < np) {
-        const float2 v = pr[(sp * slab >> 1) + c];
-        acc[j].x += v.x;
-        acc[j].y += v.y;
-      }
-    }
+    const float2 v = pr[sp * slab2];
+    acc.x += v.x;
+    acc.y += v.y;
   }
   float2* xr = (float2*)((float*)epi.out + (long long)r * epi.ldc);
-  const float2* b2 = (const float2*)epi.bias;
   float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int c = tid + 256 * j;
-    if (c < np) {
-      float2 v = acc[j];
-      if (b2) {
-        const float2 bb = b2[c];
-        v.x += bb.x;
-        v.y += bb.y;
-      }
-      float2 xv = xr[c];
-      xv.x += v.x;
-      xv.y += v.y;
-      xr[c] = xv;
-      acc[j] = xv;
-      s += xv.x + xv.y;
+  if (act) {
+    if (epi.bias) {
+      const float2 bb = ((const float2*)epi.bias)[c];
+      acc.x += bb.x;
+      acc.y += bb.y;
     }
+    float2 xv = xr[c];
+    xv.x += acc.x;
+    xv.y += acc.y;
+    xr[c] = xv;
+    acc = xv;
+    s = xv.x + xv.y;
   }
   s = wave_sum(s);
   if (lane == 0) red[0][wid] = s;
   __syncthreads();
-  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)N;
+  float tot = 0.f;
+  for (int i = 0; i < nw; ++i) tot += red[0][i];
+  const float mean = tot / (float)N;
   float q = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int c = tid + 256 * j;
-    if (c < np) {
-      const float a = acc[j].x - mean, b = acc[j].y - mean;
-      q += a * a + b * b;
-    }
+  if (act) {
+    const float a = acc.x - mean, b = acc.y - mean;
+    q = a * a + b * b;
   }
   q = wave_sum(q);
   if (lane == 0) red[1][wid] = q;
   __syncthreads();
-  const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)N + 1e-5f);
-  bf16x2* yr = (bf16x2*)(epi.ln_out + (long long)r * epi.ln_ld);
-  const float2* g2 = (const float2*)epi.ln_g;
-  const float2* lb2 = (const float2*)epi.ln_b;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int c = tid + 256 * j;
-    if (c < np) {
-      const float2 gg = g2[c], bb = lb2[c];
-      bf16x2 o;
-      o[0] = f2bf((acc[j].x - mean) * rstd * gg.x + bb.x);
-      o[1] = f2bf((acc[j].y - mean) * rstd * gg.y + bb.y);
-      yr[c] = o;
-    }
+  float qt = 0.f;
+  for (int i = 0; i < nw; ++i) qt += red[1][i];
+  const float rstd = rsqrtf(qt / (float)N + 1e-5f);
+  if (act) {
+    const float2 gg = ((const float2*)epi.ln_g)[c], bb = ((const float2*)epi.ln_b)[c];
+    bf16x2 o;
+    o[0] = f2bf((acc.x - mean) * rstd * gg.x + bb.x);
+    o[1] = f2bf((acc.y - mean) * rstd * gg.y + bb.y);
+    ((bf16x2*)(epi.ln_out + (long long)r * epi.ln_ld))[c] = o;
   }
 }
 
 static void launch_resid_ln_reduce(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st) {
   if (N % 2 != 0 || N > 2048) throw std::runtime_error("resid_ln_reduce: unsupported width " + std::to_string(N));
-  dim3 grid(M), block(256);
-  if (N <= 512) hipLaunchKernelGGL(resid_ln_reduce_kernel<1>, grid, block, 0, st, part, splitk, M, N, epi);
-  else if (N <= 1024) hipLaunchKernelGGL(resid_ln_reduce_kernel<2>, grid, block, 0, st, part, splitk, M, N, epi);
-  else if (N <= 1536) hipLaunchKernelGGL(resid_ln_reduce_kernel<3>, grid, block, 0, st, part, splitk, M, N, epi);
-  else hipLaunchKernelGGL(resid_ln_reduce_kernel<4>, grid, block, 0, st, part, splitk, M, N, epi);
+  const int threads = ((N / 2 + 63) / 64) * 64;
+  hipLaunchKernelGGL(resid_ln_reduce_kernel, dim3(M), dim3(threads), 0, st, part, splitk, M, N, epi);
   WM_LAUNCH_CHECK("resid_ln_reduce_kernel");
 }
 
@@ -444,7 +432,8 @@ void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int
     launch_layernorm((const float*)epi.out, epi.ldc, nullptr, M, N, epi.ln_g, epi.ln_b, epi.ln_out, epi.ln_ld, st);
     return;
   }
-  if (big_enabled && gemm_big_applicable(M, N, K)) {
+  const bool vec4 = epi.ldc % 4 == 0 && (epi.rpb == 0 || epi.bstride % 4 == 0);   // 4-column vector epilogue
+  if (big_enabled && vec4 && gemm_big_applicable(M, N, K)) {
     launch_gemm_big(a, w, ldw, M, N, K, epi, st);
     return;
   }

@@ -56,3 +56,79 @@ __device__ __forceinline__ void apply_epi(const GemmEpi& epi, int row, int col, 
       break;
   }
 }
+
+// Four consecutive output columns col0..col0+3 of one row (col0 % 4 == 0, col0 + 3 < N): the same
+// arithmetic as four apply_epi calls, stored as one 8-B (bf16) or 16-B (f32) access.  Used by kernels whose
+// MFMA operands are swapped (C^T fragments: each lane holds 4 consecutive columns of one row).
+template <int KIND>
+__device__ __forceinline__ void apply_epi4(const GemmEpi& epi, int row, int col0, f32x4 acc) {
+  f32x4 v = acc;
+  if (epi.bias) {
+    const f32x4 b = *(const f32x4*)(epi.bias + col0);
+    v += b;
+  }
+  switch (KIND) {
+    case EPI_BF16: {
+      if (epi.act == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      }
+      long long o = epi.rpb ? (long long)(row / epi.rpb) * epi.bstride + (long long)(row % epi.rpb + epi.roff) * epi.ldc
+                            : (long long)row * epi.ldc;
+      bf16x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = f2bf(v[e]);
+      *(bf16x4*)((bf16*)epi.out + o + col0) = r;
+      break;
+    }
+    case EPI_RESID_F32: {
+      f32x4* p = (f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0);
+      *p = *p + v;
+      break;
+    }
+    case EPI_GELU_POS_F32: {
+      const int t = row % epi.rpb;
+      const f32x4 pe = *(const f32x4*)(epi.pos + (long long)t * epi.ldc + col0);
+      f32x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = gelu_erf(v[e]) + pe[e];
+      *(f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0) = r;
+      break;
+    }
+    case EPI_F32: {
+      *(f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0) = v;
+      break;
+    }
+    case EPI_DEC_QKV: {
+      const int d = epi.d;
+      bf16x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = f2bf(v[e]);
+      if (col0 < d) {
+        *(bf16x4*)((bf16*)epi.out + (long long)row * epi.ldc + col0) = r;
+      } else {
+        const int c2 = col0 - d;
+        const int kv = c2 >= d;
+        const int cc = kv ? c2 - d : c2;
+        const int h = cc / epi.head_dim, e2 = cc - h * epi.head_dim;
+        const long long slot = (((long long)epi.row_hyp[row] * epi.n_head + h) * epi.n_ctx + epi.row_pos[row]) * epi.head_dim + e2;
+        *(bf16x4*)((kv ? epi.vcache : epi.kcache) + slot) = r;
+      }
+      break;
+    }
+    case EPI_CROSS_KV: {
+      const int d = epi.d, hd = epi.head_dim;
+      const int l2 = col0 / d, cc = col0 - l2 * d;
+      const int h = cc / hd, e2 = cc - h * hd;
+      const int b = row / epi.rpb, t = row - b * epi.rpb;
+      const long long o = ((((long long)l2 * epi.n_slots + epi.slot0 + b) * epi.n_head + h) * epi.rpb + t) * hd + e2;
+      bf16x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = f2bf(v[e]);
+      *(bf16x4*)((bf16*)epi.out + o) = r;
+      break;
+    }
+    default:
+      break;
+  }
+}

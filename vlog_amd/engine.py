@@ -134,8 +134,19 @@ class GpuEngine:
     def stream_ptr(self) -> C.c_void_p:
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def profile(self, enable: bool) -> None:
-        _capi.check(self.lib.wm_profile(self.h, int(enable)), "wm_profile")
+    def profile(self, enable: bool, classes: Optional[Sequence[str]] = None) -> None:
+        """Reset + enable the built-in event profiler (all classes, or only `classes`); False disables."""
+        if not enable:
+            _capi.check(self.lib.wm_profile_select(self.h, 0), "wm_profile_select")
+            return
+        if classes is None:
+            _capi.check(self.lib.wm_profile(self.h, 1), "wm_profile")
+            return
+        names = [self.lib.wm_profile_name(c).decode() for c in range(self.lib.wm_profile_classes())]
+        mask = 0
+        for n in classes:
+            mask |= 1 << names.index(n)
+        _capi.check(self.lib.wm_profile_select(self.h, mask), "wm_profile_select")
 
     def profile_read(self) -> Dict[str, dict]:
         out = {}
