@@ -13,6 +13,7 @@
 // the weight-bound GEMMs, which read the weights once per step regardless).
 #include "common.h"
 #include <hip/hip_ext.h>
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -192,6 +193,154 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
   out[(long long)row * ldo + h * HD + e] = f2bf(o / L);
 }
 
+// ------------------------------------------------------------------------------------------------------
+// Cross-attention, single pass (flash decoding) over RG query rows that share one window slot — the
+// beam hypotheses of a window, or the prompt positions of a prefill — so each (slot, head) K/V panel is
+// streamed from HBM once per group instead of once per row.  One 256-thread block per (group, head[, key
+// split]); 8 lanes x 16 B cover one 128-B key row, each lane group of 8 lanes takes every 8th key of its
+// wave, and every lane issues the K AND V rows of 4 keys before using any (8 x 16 B in flight per lane).
+// Per (row, lane group) an online softmax keeps (m, l, o[8]); groups merge by xor-shuffles, waves through
+// LDS.  With splits > 1 the (m, l, o) partials go to cross_combine_kernel (per row, as the legacy path).
+template <int RG>
+__global__ __launch_bounds__(256) void cross_attn_group_kernel(DecAttnArgs a) {
+  __shared__ float s_m[4][RG], s_l[4][RG];
+  __shared__ float s_o[4][RG][HD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int sub = lane & 7, g = lane >> 3;
+  const int H = a.H;
+  const int grp = blockIdx.x / H, h = blockIdx.x - grp * H;
+  const int split = blockIdx.y;
+  const int row0 = grp * RG;
+  bool live[RG];
+  bool any = false;
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    live[r] = !(a.done && a.done[a.row_hyp[row0 + r]]);
+    any |= live[r];
+  }
+  if (!any) return;
+  const int chunk = (a.T + a.splits - 1) / a.splits;
+  const int k0 = split * chunk;
+  const int nk = min(a.T, k0 + chunk) - k0;
+  const long long off = ((long long)a.hyp_slot[a.row_hyp[row0]] * H + h) * ((long long)a.T * HD) + (long long)k0 * HD;
+  const bf16* K = a.kbase + off + sub * 8;
+  const bf16* V = a.vbase + off + sub * 8;
+  if (a.stat && tid == 0) atomicAdd(a.stat, (unsigned long long)(nk * 2 * HD * 2 + RG * 2 * HD * 2));
+
+  float qf[RG][8];
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    load8(a.q + (long long)(row0 + r) * a.ldq + h * HD + sub * 8, qf[r]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qf[r][i] *= a.scale_log2;
+  }
+  float m[RG], l[RG], o[RG][8];
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[r][i] = 0.f;
+  }
+  for (int kb = 0; kb < nk; kb += 128) {
+    bf16x8 kr[4], vr[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = kb + u * 32 + wv * 8 + g;
+      ok[u] = p < nk;
+      const int pc = ok[u] ? p : 0;
+      kr[u] = *(const bf16x8*)(K + (long long)pc * HD);
+      vr[u] = *(const bf16x8*)(V + (long long)pc * HD);
+    }
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      float sc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d = fmaf(qf[r][i], bf2f(kr[u][i]), d);
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        sc[u] = ok[u] ? d : -INFINITY;
+      }
+      const float mx = fmaxf(fmaxf(m[r], fmaxf(sc[0], sc[1])), fmaxf(sc[2], sc[3]));
+      const float ms = mx == -INFINITY ? 0.f : mx;
+      const float corr = exp2f(m[r] - ms);
+      float pu[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pu[u] = exp2f(sc[u] - ms);
+      l[r] = l[r] * corr + ((pu[0] + pu[1]) + (pu[2] + pu[3]));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float x = o[r][i] * corr;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x = fmaf(pu[u], bf2f(vr[u][i]), x);
+        o[r][i] = x;
+      }
+      m[r] = mx;
+    }
+  }
+  // merge the 8 lane groups of the wave (same sub, different keys)
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+#pragma unroll
+    for (int off2 = 8; off2 < 64; off2 <<= 1) {
+      const float mo = __shfl_xor(m[r], off2, 64);
+      const float lo = __shfl_xor(l[r], off2, 64);
+      const float M = fmaxf(m[r], mo);
+      const float Ms = M == -INFINITY ? 0.f : M;
+      const float ca = exp2f(m[r] - Ms), cb = exp2f(mo - Ms);
+      l[r] = l[r] * ca + lo * cb;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float oo = __shfl_xor(o[r][i], off2, 64);
+        o[r][i] = o[r][i] * ca + oo * cb;
+      }
+      m[r] = M;
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s_o[wv][r][sub * 8 + i] = o[r][i];
+      if (sub == 0) {
+        s_m[wv][r] = m[r];
+        s_l[wv][r] = l[r];
+      }
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < RG * HD; idx += 256) {
+    const int r = idx / HD, e = idx - r * HD;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][r]);
+    const float Ms = M == -INFINITY ? 0.f : M;
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float c = exp2f(s_m[w][r] - Ms);
+      L += s_l[w][r] * c;
+      O += s_o[w][r][e] * c;
+    }
+    const int row = row0 + r;
+    if (a.splits == 1) {
+      if (!(a.done && a.done[a.row_hyp[row]])) a.out[(long long)row * a.ldo + h * HD + e] = f2bf(O / L);
+    } else {
+      const long long pi = ((long long)row * H + h) * a.splits + split;
+      a.part_o[pi * HD + e] = O;
+      if (e == 0) { a.part_m[pi] = M; a.part_l[pi] = L; }
+    }
+  }
+}
+
+template <int RG>
+static void launch_group(dim3 grid, const DecAttnArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+  if (ev0) hipExtLaunchKernelGGL(cross_attn_group_kernel<RG>, grid, dim3(256), 0, st, ev0, ev1, 0, a);
+  else hipLaunchKernelGGL(cross_attn_group_kernel<RG>, grid, dim3(256), 0, st, a);
+}
+
 static void launch_k(bool self, dim3 grid, const DecAttnArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (ev0) {
     if (self) hipExtLaunchKernelGGL(dec_attn_kernel<true>, grid, dim3(256), 0, st, ev0, ev1, 0, a);
@@ -216,22 +365,52 @@ void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* 
 }
 
 void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf16* vbase, int T, const int* hyp_slot,
-                       const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H, int splits,
+                       const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H, int group,
                        float* part_m, float* part_l, float* part_o, float* probs, const int* head_map, int n_align,
                        unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
-  if (T > CT_MAX * splits) throw std::runtime_error("cross_attn: too many keys per split");
-  if (probs && splits != 1) throw std::runtime_error("cross_attn: attention capture needs splits == 1");
   DecAttnArgs a{};
   a.q = q; a.ldq = ldq; a.kbase = kbase; a.vbase = vbase; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
-  a.out = out; a.ldo = ldo; a.H = H; a.T = T; a.n_ctx = T; a.splits = splits;
+  a.out = out; a.ldo = ldo; a.H = H; a.T = T; a.n_ctx = T;
   a.part_m = part_m; a.part_l = part_l; a.part_o = part_o; a.probs = probs; a.head_map = head_map; a.n_align = n_align;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;
-  launch_k(false, dim3(rows * H, splits), a, st, ev0, ev1);
-  WM_LAUNCH_CHECK("dec_attn_kernel<cross>");
+  if (probs) {        // attention capture (word alignment): the two-pass kernel keeps the probabilities
+    if (T > CT_MAX) throw std::runtime_error("cross_attn: too many keys for capture");
+    a.splits = 1;
+    launch_k(false, dim3(rows * H, 1), a, st, ev0, ev1);
+    WM_LAUNCH_CHECK("dec_attn_kernel<cross>");
+    return;
+  }
+  // rows [k RG, (k+1) RG) share a slot: RG = the largest divisor of `group` (rows sharing a slot,
+  // contiguous) that is <= 8 and divides rows
+  int rg = 1;
+  for (int c = 8; c >= 1; --c)
+    if (group % c == 0 && rows % c == 0) { rg = c; break; }
+  const int blocks = rows / rg * H;
+  int splits = (2048 + blocks - 1) / blocks;
+  splits = std::max(1, std::min(splits, std::min(16, T / 128)));
+  a.splits = splits;
+  const dim3 grid(blocks, splits);
+  // events (profiler): start on the attention kernel, stop on the last kernel of the pair
+  hipEvent_t e0 = ev0, e1 = splits == 1 ? ev1 : nullptr;
+  switch (rg) {
+    case 1: launch_group<1>(grid, a, st, e0, e1); break;
+    case 2: launch_group<2>(grid, a, st, e0, e1); break;
+    case 3: launch_group<3>(grid, a, st, e0, e1); break;
+    case 4: launch_group<4>(grid, a, st, e0, e1); break;
+    case 5: launch_group<5>(grid, a, st, e0, e1); break;
+    case 6: launch_group<6>(grid, a, st, e0, e1); break;
+    case 7: launch_group<7>(grid, a, st, e0, e1); break;
+    default: launch_group<8>(grid, a, st, e0, e1); break;
+  }
+  WM_LAUNCH_CHECK("cross_attn_group_kernel");
   if (splits > 1) {
-    hipLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, part_m, part_l, part_o, row_hyp, done,
-                       out, ldo, H, splits);
+    if (ev1)
+      hipExtLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, nullptr, ev1, 0, part_m, part_l,
+                            part_o, row_hyp, done, out, ldo, H, splits);
+    else
+      hipLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, part_m, part_l, part_o, row_hyp, done,
+                         out, ldo, H, splits);
     WM_LAUNCH_CHECK("cross_combine_kernel");
   }
 }

@@ -379,19 +379,12 @@ void ensure_step(wm_engine* e, int rows, int logit_rows) {
   e->d_logit_rows.ensure((size_t)logit_rows * 4);
 }
 
-int cross_splits(int rows, int H) {
-  int pairs = rows * H;
-  int s = (2048 + pairs - 1) / pairs;
-  if (s < 1) s = 1;
-  if (s > 16) s = 16;
-  return s;
-}
-
 // One decoder pass over `rows` rows; logits for the n_logit rows listed in logit_rows (device) go to
 // `logits`.  Optional cross-attention capture (align): head_map per layer computed by caller.
 void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos, const int* row_hyp, const int* done,
                   const int* lin, const int* logit_rows, int n_logit, float* logits,
-                  const std::vector<std::vector<int>>* align_map, int n_align, float* attn, hipStream_t st) {
+                  const std::vector<std::vector<int>>* align_map, int n_align, float* attn, int cross_group,
+                  hipStream_t st) {
   const auto& m = e->dm;
   const int d = m.n_state, H = m.n_head, L = m.n_dec_layer, T = m.n_audio_ctx, C = m.n_text_ctx;
   float* x = e->s_x.as<float>();
@@ -403,7 +396,6 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
   const size_t ckv_layer = (size_t)e->n_slots * H * T * 64;
   bf16* skv = e->skv.as<bf16>();
   bf16* ckv = e->ckv.as<bf16>();
-  const int splits = attn ? 1 : cross_splits(rows, H);
   {
     ProfScope ps(e, P_DEC_OTHER, st);
     launch_embed(row_tok, row_pos, e->Wb("dec.embed"), e->Wf("dec.pos"), x, rows, d, st);
@@ -449,11 +441,11 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
       }
     }
     {
-      ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, splits == 1);
+      ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
       launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
-                        e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, splits, e->s_pm.as<float>(),
+                        e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, cross_group, e->s_pm.as<float>(),
                         e->s_pl.as<float>(), e->s_po.as<float>(), probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st,
-                        splits == 1 ? ps.a : nullptr, splits == 1 ? ps.b : nullptr);
+                        ps.a, ps.b);
     }
     if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
     {
@@ -591,7 +583,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   }
   float* logits = e->s_logits.as<float>();
   decoder_pass(e, rows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_prow_hyp.as<int>(), nullptr,
-               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, logits, nullptr, 0, nullptr, st);
+               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, logits, nullptr, 0, nullptr, per * P, st);
   if (a->sot_index >= 0) launch_no_speech(logits + (size_t)NH * V, V, V, NH, m.no_speech, e->d_ns.as<float>(), st);
 
   SearchParams sp;
@@ -632,7 +624,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     }
     // logits rows of a decode step are the hypotheses themselves
     decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                 e->d_lin.as<int>(), e->d_row_hyp.as<int>(), NH, logits, nullptr, 0, nullptr, st);
+                 e->d_lin.as<int>(), e->d_row_hyp.as<int>(), NH, logits, nullptr, 0, nullptr, per, st);
     select(step);
     ++steps;
   }
@@ -735,7 +727,7 @@ void forward(wm_engine* e, int n_seq, const int* h_slots, int S, const int* h_to
   HIP_OK(hipMemcpyAsync(e->d_lin.p, lin.data(), lin.size() * 4, hipMemcpyHostToDevice, st));
   decoder_pass(e, rows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_prow_hyp.as<int>(), nullptr,
                e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, d_logits, n_align ? &amap : nullptr, n_align,
-               n_align ? d_attn : nullptr, st);
+               n_align ? d_attn : nullptr, S, st);
   HIP_OK(hipStreamSynchronize(st));
 }
 
