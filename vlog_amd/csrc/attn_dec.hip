@@ -35,7 +35,7 @@ struct DecAttnArgs {
   float* part_m; float* part_l; float* part_o;
   float* probs; const int* head_map; int n_align;
   float scale_log2;
-  unsigned long long* stat;
+  unsigned long long* stat;   // profiler byte counter: STAT_SLOTS slots, summed on read (no hot atomic)
 };
 
 #define CT_MAX 1536
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttnArgs a) {
     K = a.kbase + off;
     V = a.vbase + off;
   }
-  if (a.stat && tid == 0) atomicAdd(a.stat, (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
+  if (a.stat && tid == 0) atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
   const long long hstride = (long long)H * a.n_ctx * HD;    // SELF: elements per physical hypothesis
   const int sub = lane & 7, g = lane >> 3;
   float qf[8];
@@ -225,7 +225,8 @@ __global__ __launch_bounds__(256) void cross_attn_group_kernel(DecAttnArgs a) {
   const long long off = ((long long)a.hyp_slot[a.row_hyp[row0]] * H + h) * ((long long)a.T * HD) + (long long)k0 * HD;
   const bf16* K = a.kbase + off + sub * 8;
   const bf16* V = a.vbase + off + sub * 8;
-  if (a.stat && tid == 0) atomicAdd(a.stat, (unsigned long long)(nk * 2 * HD * 2 + RG * 2 * HD * 2));
+  if (a.stat && tid == 0)
+    atomicAdd(a.stat + ((blockIdx.x + blockIdx.y) & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + RG * 2 * HD * 2));
 
   float qf[RG][8];
 #pragma unroll
@@ -341,6 +342,103 @@ static void launch_group(dim3 grid, const DecAttnArgs& a, hipStream_t st, hipEve
   else hipLaunchKernelGGL(cross_attn_group_kernel<RG>, grid, dim3(256), 0, st, a);
 }
 
+// ------------------------------------------------------------------------------------------------------
+// Self-attention, single pass: one WAVE per (row, head), 4 per block, no LDS and no barriers.  A row's
+// keys are positions 0..pos of its hypothesis, key p read from physical slot lin[hyp][p] (beam lineage).
+// Per 64-key chunk each lane fetches one lineage index and the 8 lane groups get theirs by shuffle; every
+// lane then issues the K and V rows of 8 keys (16 x 16 B in flight) before using them.  Online softmax
+// per lane group, merged by xor-shuffles; lanes 0-7 store the 64 outputs (16 B each).
+__global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int n_pairs) {
+  const int lane = threadIdx.x & 63;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= n_pairs) return;
+  const int sub = lane & 7, g = lane >> 3;
+  const int H = a.H;
+  const int row = pair / H, h = pair - row * H;
+  const int hyp = a.row_hyp[row];
+  if (a.done && a.done[hyp]) return;
+  const int nk = a.row_pos[row] + 1;
+  const int* lrow = a.lin ? a.lin + (long long)hyp * a.n_ctx : nullptr;
+  const long long hstride = (long long)H * a.n_ctx * HD;
+  const bf16* K = a.kbase + (long long)h * a.n_ctx * HD + sub * 8;
+  const bf16* V = a.vbase + (long long)h * a.n_ctx * HD + sub * 8;
+  if (a.stat && lane == 0) atomicAdd(a.stat + (pair & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
+  float qf[8];
+  load8(a.q + (long long)row * a.ldq + h * HD + sub * 8, qf);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) qf[i] *= a.scale_log2;
+  float m = -INFINITY, l = 0.f, o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = 0.f;
+  for (int kb = 0; kb < nk; kb += 64) {
+    const int pl = kb + lane;
+    const int phl = (lrow && pl < nk) ? lrow[pl] : hyp;
+    bf16x8 kr[8], vr[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = kb + u * 8 + g;
+      const int ph = __shfl(phl, u * 8 + g, 64);
+      const int pc = p < nk ? p : 0;
+      const long long ro = (long long)ph * hstride + (long long)pc * HD;
+      kr[u] = *(const bf16x8*)(K + ro);
+      vr[u] = *(const bf16x8*)(V + ro);
+    }
+    float sc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d = fmaf(qf[i], bf2f(kr[u][i]), d);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      sc[u] = (kb + u * 8 + g) < nk ? d : -INFINITY;
+    }
+    float mx = m;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mx = fmaxf(mx, sc[u]);
+    const float ms = mx == -INFINITY ? 0.f : mx;
+    const float corr = exp2f(m - ms);
+    float pu[8], ps = 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      pu[u] = exp2f(sc[u] - ms);
+      ps += pu[u];
+    }
+    l = l * corr + ps;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float x = o[i] * corr;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x = fmaf(pu[u], bf2f(vr[u][i]), x);
+      o[i] = x;
+    }
+    m = mx;
+  }
+#pragma unroll
+  for (int off2 = 8; off2 < 64; off2 <<= 1) {
+    const float mo = __shfl_xor(m, off2, 64);
+    const float lo = __shfl_xor(l, off2, 64);
+    const float M = fmaxf(m, mo);
+    const float Ms = M == -INFINITY ? 0.f : M;
+    const float ca = exp2f(m - Ms), cb = exp2f(mo - Ms);
+    l = l * ca + lo * cb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float oo = __shfl_xor(o[i], off2, 64);
+      o[i] = o[i] * ca + oo * cb;
+    }
+    m = M;
+  }
+  if (g == 0) {
+    const float inv = 1.0f / l;
+    bf16x8 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = f2bf(o[i] * inv);
+    *(bf16x8*)(a.out + (long long)row * a.ldo + h * HD + sub * 8) = r;
+  }
+}
+
 static void launch_k(bool self, dim3 grid, const DecAttnArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (ev0) {
     if (self) hipExtLaunchKernelGGL(dec_attn_kernel<true>, grid, dim3(256), 0, st, ev0, ev1, 0, a);
@@ -355,13 +453,15 @@ void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* 
                       const int* row_pos, const int* done, bf16* out, long long ldo, int rows, int H, int n_ctx,
                       unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
-  if (n_ctx > CT_MAX) throw std::runtime_error("self_attn: n_ctx too large");
   DecAttnArgs a{};
   a.q = q; a.ldq = ldq; a.kbase = kc; a.vbase = vc; a.row_hyp = row_hyp; a.row_pos = row_pos; a.done = done; a.lin = lin;
   a.out = out; a.ldo = ldo; a.H = H; a.T = n_ctx; a.n_ctx = n_ctx; a.splits = 1;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;
-  launch_k(true, dim3(rows * H, 1), a, st, ev0, ev1);
-  WM_LAUNCH_CHECK("dec_attn_kernel<self>");
+  const int n_pairs = rows * H;
+  const dim3 grid((n_pairs + 3) / 4);
+  if (ev0) hipExtLaunchKernelGGL(self_attn_wave_kernel, grid, dim3(256), 0, st, ev0, ev1, 0, a, n_pairs);
+  else hipLaunchKernelGGL(self_attn_wave_kernel, grid, dim3(256), 0, st, a, n_pairs);
+  WM_LAUNCH_CHECK("self_attn_wave_kernel");
 }
 
 void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf16* vbase, int T, const int* hyp_slot,
@@ -387,7 +487,9 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
   for (int c = 8; c >= 1; --c)
     if (group % c == 0 && rows % c == 0) { rg = c; break; }
   const int blocks = rows / rg * H;
-  int splits = (2048 + blocks - 1) / blocks;
+  // RG = 1 is HBM-bound: split keys until the last round of resident blocks (~1280 at RG = 1) is a small
+  // fraction; RG > 1 does RG x the VALU work per byte, so only fill the chip (~2048 blocks)
+  int splits = ((rg == 1 ? 10240 : 2048) + blocks - 1) / blocks;
   splits = std::max(1, std::min(splits, std::min(16, T / 128)));
   a.splits = splits;
   const dim3 grid(blocks, splits);

@@ -12,6 +12,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 #define WAVE 64
+#define STAT_SLOTS 256   // profiler byte counters per kernel class (spread to avoid one hot atomic)
 
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }

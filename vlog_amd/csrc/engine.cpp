@@ -129,7 +129,7 @@ struct wm_engine {
     ev_pool.pop_back();
     return ev;
   }
-  unsigned long long* dstat(int cls) { return (prof_on && ((prof_mask >> cls) & 1u)) ? prof_dbytes.as<unsigned long long>() + cls : nullptr; }
+  unsigned long long* dstat(int cls) { return (prof_on && ((prof_mask >> cls) & 1u)) ? prof_dbytes.as<unsigned long long>() + (size_t)cls * STAT_SLOTS : nullptr; }
 
   const Slot& slot(const std::string& n) const {
     auto it = slots.find(n);
@@ -979,8 +979,8 @@ int wm_profile_select(wm_engine* e, uint32_t class_mask) {
       e->prof_flops[c] = 0;
       e->prof_bytes[c] = 0;
     }
-    e->prof_dbytes.ensure(P_N * sizeof(unsigned long long));
-    HIP_OK(hipMemset(e->prof_dbytes.p, 0, P_N * sizeof(unsigned long long)));
+    e->prof_dbytes.ensure((size_t)P_N * STAT_SLOTS * sizeof(unsigned long long));
+    HIP_OK(hipMemset(e->prof_dbytes.p, 0, (size_t)P_N * STAT_SLOTS * sizeof(unsigned long long)));
     e->prof_mask = class_mask;
     e->prof_on = true;
   });
@@ -998,12 +998,16 @@ int wm_profile_read(wm_engine* e, int32_t cls, int64_t* launches, double* ms, do
       HIP_OK(hipEventElapsedTime(&x, pr.first, pr.second));
       t += x;
     }
-    unsigned long long db[P_N] = {0};
-    if (e->prof_dbytes.p) HIP_OK(hipMemcpy(db, e->prof_dbytes.p, sizeof(db), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> slots(STAT_SLOTS, 0);
+    if (e->prof_dbytes.p)
+      HIP_OK(hipMemcpy(slots.data(), e->prof_dbytes.as<unsigned long long>() + (size_t)cls * STAT_SLOTS,
+                       STAT_SLOTS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    double dbytes = 0;
+    for (auto v : slots) dbytes += (double)v;
     *launches = (int64_t)e->prof_ev[cls].size();
     *ms = t;
     *flops = e->prof_flops[cls];
-    *bytes = e->prof_bytes[cls] + (double)db[cls];
+    *bytes = e->prof_bytes[cls] + dbytes;
   });
 }
 

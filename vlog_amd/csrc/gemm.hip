@@ -350,12 +350,14 @@ static void dispatch_skinny(const GemmA& a, const bf16* w, long long ldw, int M,
   else if (M <= 64) run_skinny<4, 512, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
   else if (M <= 128) run_skinny<8, 256, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
   else if (M <= 160) run_skinny<10, 256, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else run_skinny<16, 128, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 256) run_skinny<16, 128, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 320) run_skinny<20, 128, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_skinny<32, 64, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
 static bool try_skinny(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                        size_t ws_bytes, hipStream_t st) {
-  if (M > 256 || !ws) return false;
+  if (M > 512 || !ws) return false;
   int splitk, kr;
   if (!skinny_plan(M, N, K, ws_bytes, &splitk, &kr)) return false;
   switch (epi.kind) {
