@@ -135,6 +135,12 @@ int64_t wm_device_bytes(wm_engine* e);
 int32_t wm_profile_classes(void);
 const char* wm_profile_name(int32_t cls);
 int wm_profile(wm_engine* e, int32_t enable);
+/* Engine options (no reference counterpart: scheduling knobs of this build only).
+ *   "decode_split" (default 0): decode steps with >= 32 rows run as two row slices on two streams, one
+ *   slice's weight GEMMs overlapping the other's cross-attention.  Results are bit-identical
+ *   either way; off by default because the overlap measured slower on MI355X (the GEMM blocks queue behind
+ *   the cross-attention blocks). */
+int wm_set_option(wm_engine* e, const char* key, int64_t value);
 /* As wm_profile(e, 1) but only the classes whose bit is set in class_mask are timed (0 disables), so a
  * timed run can keep events on the dominant kernel alone. */
 int wm_profile_select(wm_engine* e, uint32_t class_mask);

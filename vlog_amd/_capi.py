@@ -18,7 +18,7 @@ SYMBOLS = (
     "wm_create", "wm_destroy", "wm_last_error", "wm_abi_version", "wm_set_weight", "wm_weights_complete",
     "wm_logmel", "wm_logmel_finalize", "wm_encode", "wm_reserve", "wm_cross_kv", "wm_generate", "wm_forward",
     "wm_frame_energy", "wm_align", "wm_dtw", "wm_device_bytes", "wm_profile_classes", "wm_profile_name", "wm_profile", "wm_profile_select",
-    "wm_profile_read",
+    "wm_profile_read", "wm_set_option",
 )
 
 
@@ -77,6 +77,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "wm_profile_name": (C.c_char_p, [i32]),
         "wm_profile": (C.c_int, [vp, i32]),
         "wm_profile_select": (C.c_int, [vp, C.c_uint32]),
+        "wm_set_option": (C.c_int, [vp, C.c_char_p, i64]),
         "wm_profile_read": (C.c_int, [vp, i32, C.POINTER(i64), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),
     }

@@ -467,8 +467,9 @@ void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* 
 void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf16* vbase, int T, const int* hyp_slot,
                        const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H, int group,
                        float* part_m, float* part_l, float* part_o, float* probs, const int* head_map, int n_align,
-                       unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                       int plan_rows, unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
+  if (plan_rows < rows) plan_rows = rows;
   DecAttnArgs a{};
   a.q = q; a.ldq = ldq; a.kbase = kbase; a.vbase = vbase; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
   a.out = out; a.ldo = ldo; a.H = H; a.T = T; a.n_ctx = T;
@@ -488,8 +489,11 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
     if (group % c == 0 && rows % c == 0) { rg = c; break; }
   const int blocks = rows / rg * H;
   // RG = 1 is HBM-bound: split keys until the last round of resident blocks (~1280 at RG = 1) is a small
-  // fraction; RG > 1 does RG x the VALU work per byte, so only fill the chip (~2048 blocks)
-  int splits = ((rg == 1 ? 10240 : 2048) + blocks - 1) / blocks;
+  // fraction; RG > 1 does RG x the VALU work per byte, so only fill the chip (~2048 blocks).  The split count
+  // follows `plan_rows` (the whole pass), not this launch's rows, so a row's summation order — and so its
+  // result, bit for bit — does not depend on how the pass was sliced into launches.
+  const int plan_blocks = plan_rows / rg * H;
+  int splits = ((rg == 1 ? 10240 : 2048) + plan_blocks - 1) / plan_blocks;
   splits = std::max(1, std::min(splits, std::min(16, T / 128)));
   a.splits = splits;
   const dim3 grid(blocks, splits);

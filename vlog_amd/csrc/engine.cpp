@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -36,8 +37,8 @@ void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
 void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const int*, const int*, const int*, const int*,
                       bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
-                       long long, int, int, int, float*, float*, float*, float*, const int*, int, unsigned long long*,
-                       hipStream_t, hipEvent_t, hipEvent_t);
+                       long long, int, int, int, float*, float*, float*, float*, const int*, int, int,
+                       unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
@@ -89,6 +90,12 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+// Decoder weight pointers per layer (resolved once: the arena layout is fixed at wm_create).
+struct DecLayerW {
+  const bf16 *qkv_w, *out_w, *cq_w, *cout_w, *fc1_w, *fc2_w;
+  const float *qkv_b, *out_b, *cq_b, *cout_b, *fc1_b, *fc2_b, *ln1_w, *ln1_b, *ln2_w, *ln2_b, *ln3_w, *ln3_b;
+};
+
 struct wm_engine {
   wm_model_dims dm;
   int device;
@@ -116,7 +123,12 @@ struct wm_engine {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[P_N];
   std::vector<hipEvent_t> ev_pool;
   double prof_flops[P_N] = {0}, prof_bytes[P_N] = {0};
-  DevBuf gemm_ws;            // split-K partial slabs
+  DevBuf gemm_ws, gemm_ws2;  // split-K partial slabs (per decoder slice stream)
+  // two-slice decode (decoder_pass): second stream + fork/phase/join events
+  bool dec_split = false;   // measured slower on MI355X (r01: GEMMs queue behind cross-attention blocks)
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
+  std::vector<DecLayerW> dec_w;
   DevBuf a_logits, a_attn, a_next, a_probs, a_rowsum, a_z, a_mat, a_cost, a_trace, a_pi, a_pj, a_plen;
   DevBuf prof_dbytes;        // device counters (attention kernels add the bytes they actually read)
   hipEvent_t ev_get() {
@@ -379,98 +391,186 @@ void ensure_step(wm_engine* e, int rows, int logit_rows) {
   e->d_logit_rows.ensure((size_t)logit_rows * 4);
 }
 
-// One decoder pass over `rows` rows; logits for the n_logit rows listed in logit_rows (device) go to
-// `logits`.  Optional cross-attention capture (align): head_map per layer computed by caller.
+const std::vector<DecLayerW>& dec_weights(wm_engine* e) {
+  if ((int)e->dec_w.size() == e->dm.n_dec_layer) return e->dec_w;
+  e->dec_w.clear();
+  for (int l = 0; l < e->dm.n_dec_layer; ++l) {
+    const std::string p = "dec." + std::to_string(l) + ".";
+    DecLayerW w;
+    w.qkv_w = e->Wb(p + "qkv.w"); w.out_w = e->Wb(p + "out.w"); w.cq_w = e->Wb(p + "cq.w");
+    w.cout_w = e->Wb(p + "cout.w"); w.fc1_w = e->Wb(p + "fc1.w"); w.fc2_w = e->Wb(p + "fc2.w");
+    w.qkv_b = e->Wf(p + "qkv.b"); w.out_b = e->Wf(p + "out.b"); w.cq_b = e->Wf(p + "cq.b");
+    w.cout_b = e->Wf(p + "cout.b"); w.fc1_b = e->Wf(p + "fc1.b"); w.fc2_b = e->Wf(p + "fc2.b");
+    w.ln1_w = e->Wf(p + "ln1.w"); w.ln1_b = e->Wf(p + "ln1.b"); w.ln2_w = e->Wf(p + "ln2.w");
+    w.ln2_b = e->Wf(p + "ln2.b"); w.ln3_w = e->Wf(p + "ln3.w"); w.ln3_b = e->Wf(p + "ln3.b");
+    e->dec_w.push_back(w);
+  }
+  return e->dec_w;
+}
+
+// A contiguous range of decoder rows [r0, r0 + rows) of a pass over total_rows, issued on its own stream
+// with its own split-K scratch.
+struct DecSlice {
+  int r0, rows, total_rows;
+  hipStream_t st;
+  DevBuf* ws;
+};
+
+// Issues decoder layer l for one slice.  `mid` (optional) is recorded on the slice's stream right before its
+// cross-attention, which is where the second slice starts (see decoder_pass).
+void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, const int* row_hyp, const int* done,
+                   const int* lin, const std::vector<std::vector<int>>* align_map, int n_align, float* attn,
+                   int cross_group, hipEvent_t mid) {
+  const auto& m = e->dm;
+  const int d = m.n_state, H = m.n_head, L = m.n_dec_layer, T = m.n_audio_ctx, C = m.n_text_ctx;
+  const int r0 = sl.r0, rows = sl.rows;
+  hipStream_t st = sl.st;
+  float* x = e->s_x.as<float>() + (size_t)r0 * d;
+  bf16* hb = e->s_hb.as<bf16>() + (size_t)r0 * d;
+  bf16* q = e->s_q.as<bf16>() + (size_t)r0 * d;
+  bf16* ao = e->s_ao.as<bf16>() + (size_t)r0 * d;
+  bf16* ff = e->s_ff.as<bf16>() + (size_t)r0 * 4 * d;
+  row_pos += r0;
+  row_hyp += r0;
+  const size_t skv_layer = (size_t)e->n_hyp_cap * H * C * 64;      // elements per (layer, k|v)
+  const size_t ckv_layer = (size_t)e->n_slots * H * T * 64;
+  bf16* skv = e->skv.as<bf16>();
+  bf16* ckv = e->ckv.as<bf16>();
+  const auto& W = dec_weights(e)[l];
+  const size_t wsb = 64ull << 20;
+  sl.ws->ensure(wsb);
+  float* ws = sl.ws->as<float>();
+  auto gemm = [&](const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
+    const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : 2;
+    ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
+    launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
+  };
+  // residual-producing GEMMs also apply the LayerNorm that consumes the residual (EPI_RESID_LN: fused into
+  // the split-K combine on the skinny path): out -> ln2, cout -> ln3, fc2 -> next layer's ln1
+  auto resid_ln = [&](const float* g, const float* b, const float* bias) {
+    GemmEpi ep = epi_of(EPI_RESID_LN, x, d, bias);
+    ep.ln_g = g; ep.ln_b = b; ep.ln_out = hb; ep.ln_ld = d;
+    return ep;
+  };
+  bf16* kc = skv + (size_t)(2 * l) * skv_layer;
+  bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
+  {
+    GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, W.qkv_b);
+    ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
+    ep.d = d; ep.n_head = H; ep.head_dim = 64; ep.n_ctx = C;
+    gemm(amat(hb, d), W.qkv_w, d, 3 * d, d, ep);
+  }
+  {
+    ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
+    launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
+  }
+  gemm(amat(ao, d), W.out_w, d, d, d, resid_ln(W.ln2_w, W.ln2_b, W.out_b));
+  gemm(amat(hb, d), W.cq_w, d, d, d, epi_of(EPI_BF16, q, d, W.cq_b));
+  float* probs = nullptr;
+  const int* hmap = nullptr;
+  if (attn && align_map) {
+    const auto& mp = (*align_map)[l];
+    bool any = false;
+    for (int v : mp) any |= v >= 0;
+    if (any) {
+      HIP_OK(hipMemcpyAsync(e->d_head_map.p, mp.data(), H * 4, hipMemcpyHostToDevice, st));
+      probs = attn + (size_t)r0 * n_align * T;
+      hmap = e->d_head_map.as<int>();
+    }
+  }
+  if (mid) HIP_OK(hipEventRecord(mid, st));
+  {
+    const size_t po = (size_t)r0 * H * 16;
+    ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
+    launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
+                      e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, cross_group, e->s_pm.as<float>() + po,
+                      e->s_pl.as<float>() + po, e->s_po.as<float>() + po * 64, probs, hmap, n_align, sl.total_rows,
+                      e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+  }
+  if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
+  gemm(amat(ao, d), W.cout_w, d, d, d, resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
+  {
+    GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, W.fc1_b);
+    ep.act = 1;
+    gemm(amat(hb, d), W.fc1_w, d, 4 * d, d, ep);
+  }
+  if (l + 1 < L) {
+    const auto& Wn = dec_weights(e)[l + 1];
+    gemm(amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, resid_ln(Wn.ln1_w, Wn.ln1_b, W.fc2_b));
+  } else {
+    gemm(amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, epi_of(EPI_RESID_F32, x, d, W.fc2_b));
+  }
+}
+
+// One decoder pass over `rows` rows; logits for the n_logit rows listed in logit_rows (device; nullptr =
+// rows 0..n_logit-1) go to `logits`.  Optional cross-attention capture (align): head_map per layer computed
+// by caller.
+//
+// Decode steps (logit_rows == nullptr, n_logit == rows, no capture) with enough rows split the rows into two
+// slices on two streams, the second started when the first reaches its layer-0 cross-attention.  Each
+// slice then alternates a latency-bound chain of skinny weight GEMMs with an HBM-bound cross-attention,
+// and the two slices run in opposite phase: one slice's GEMM chain executes while the other streams its
+// cross-KV, so the step costs ~max(chain, cross) per layer instead of their sum.  The weights are read once
+// per slice (46 MB per layer for large-v3, against 1.15 GB of cross-KV), and every row sees exactly the
+// same arithmetic as in a one-slice pass.
 void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos, const int* row_hyp, const int* done,
                   const int* lin, const int* logit_rows, int n_logit, float* logits,
                   const std::vector<std::vector<int>>* align_map, int n_align, float* attn, int cross_group,
                   hipStream_t st) {
   const auto& m = e->dm;
-  const int d = m.n_state, H = m.n_head, L = m.n_dec_layer, T = m.n_audio_ctx, C = m.n_text_ctx;
-  float* x = e->s_x.as<float>();
-  bf16* hb = e->s_hb.as<bf16>();
-  bf16* q = e->s_q.as<bf16>();
-  bf16* ao = e->s_ao.as<bf16>();
-  bf16* ff = e->s_ff.as<bf16>();
-  const size_t skv_layer = (size_t)e->n_hyp_cap * H * C * 64;      // elements per (layer, k|v)
-  const size_t ckv_layer = (size_t)e->n_slots * H * T * 64;
-  bf16* skv = e->skv.as<bf16>();
-  bf16* ckv = e->ckv.as<bf16>();
-  {
-    ProfScope ps(e, P_DEC_OTHER, st);
-    launch_embed(row_tok, row_pos, e->Wb("dec.embed"), e->Wf("dec.pos"), x, rows, d, st);
-    launch_layernorm(x, d, nullptr, rows, d, e->Wf("dec.0.ln1.w"), e->Wf("dec.0.ln1.b"), hb, d, st);
+  const int d = m.n_state, L = m.n_dec_layer;
+  const auto& W0 = dec_weights(e)[0];
+  int h0 = (rows / 2 / cross_group) * cross_group;
+  const bool split = e->dec_split && logit_rows == nullptr && n_logit == rows && attn == nullptr && h0 >= 16 &&
+                     rows - h0 >= 16;
+  std::vector<DecSlice> sl;
+  if (split) {
+    if (!e->st2) {
+      int lo = 0, hi = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_OK(hipStreamCreateWithPriority(&e->st2, hipStreamNonBlocking, hi));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_mid, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+    }
+    sl.push_back({0, h0, rows, st, &e->gemm_ws});
+    sl.push_back({h0, rows - h0, rows, e->st2, &e->gemm_ws2});
+    HIP_OK(hipEventRecord(e->ev_fork, st));
+    HIP_OK(hipStreamWaitEvent(e->st2, e->ev_fork, 0));
+  } else {
+    sl.push_back({0, rows, rows, st, &e->gemm_ws});
   }
-  // residual-producing GEMMs also apply the LayerNorm that consumes the residual (EPI_RESID_LN: fused into
-  // the split-K combine on the skinny path): out -> ln2, cout -> ln3, fc2 -> next layer's ln1
-  auto resid_ln = [&](const std::string& ln) {
-    GemmEpi ep = epi_of(EPI_RESID_LN, x, d, nullptr);
-    ep.ln_g = e->Wf(ln + ".w"); ep.ln_b = e->Wf(ln + ".b"); ep.ln_out = hb; ep.ln_ld = d;
-    return ep;
-  };
+  for (const auto& s : sl) {
+    ProfScope ps(e, P_DEC_OTHER, s.st);
+    float* x = e->s_x.as<float>() + (size_t)s.r0 * d;
+    launch_embed(row_tok + s.r0, row_pos + s.r0, e->Wb("dec.embed"), e->Wf("dec.pos"), x, s.rows, d, s.st);
+    launch_layernorm(x, d, nullptr, s.rows, d, W0.ln1_w, W0.ln1_b, e->s_hb.as<bf16>() + (size_t)s.r0 * d, d, s.st);
+  }
   for (int l = 0; l < L; ++l) {
-    const std::string p = "dec." + std::to_string(l) + ".";
-    bf16* kc = skv + (size_t)(2 * l) * skv_layer;
-    bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
-    {
-      GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, e->Wf(p + "qkv.b"));
-      ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
-      ep.d = d; ep.n_head = H; ep.head_dim = 64; ep.n_ctx = C;
-      gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "qkv.w"), d, rows, 3 * d, d, ep, st);
-    }
-    {
-      ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
-      launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
-    }
-    {
-      GemmEpi ep = resid_ln(p + "ln2");
-      ep.bias = e->Wf(p + "out.b");
-      gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "out.w"), d, rows, d, d, ep, st);
-    }
-    gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "cq.w"), d, rows, d, d, epi_of(EPI_BF16, q, d, e->Wf(p + "cq.b")), st);
-    float* probs = nullptr;
-    const int* hmap = nullptr;
-    if (attn && align_map) {
-      const auto& mp = (*align_map)[l];
-      bool any = false;
-      for (int v : mp) any |= v >= 0;
-      if (any) {
-        HIP_OK(hipMemcpyAsync(e->d_head_map.p, mp.data(), H * 4, hipMemcpyHostToDevice, st));
-        probs = attn;
-        hmap = e->d_head_map.as<int>();
-      }
-    }
-    {
-      ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
-      launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
-                        e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, cross_group, e->s_pm.as<float>(),
-                        e->s_pl.as<float>(), e->s_po.as<float>(), probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st,
-                        ps.a, ps.b);
-    }
-    if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
-    {
-      GemmEpi ep = resid_ln(p + "ln3");
-      ep.bias = e->Wf(p + "cout.b");
-      gemm_p(e, P_DEC_GEMM, amat(ao, d), e->Wb(p + "cout.w"), d, rows, d, d, ep, st);
-    }
-    {
-      GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, e->Wf(p + "fc1.b"));
-      ep.act = 1;
-      gemm_p(e, P_DEC_GEMM, amat(hb, d), e->Wb(p + "fc1.w"), d, rows, 4 * d, d, ep, st);
-    }
-    if (l + 1 < L) {
-      GemmEpi ep = resid_ln("dec." + std::to_string(l + 1) + ".ln1");
-      ep.bias = e->Wf(p + "fc2.b");
-      gemm_p(e, P_DEC_GEMM, amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, ep, st);
-    } else {
-      gemm_p(e, P_DEC_GEMM, amat(ff, 4LL * d), e->Wb(p + "fc2.w"), 4LL * d, rows, d, 4 * d, epi_of(EPI_RESID_F32, x, d, e->Wf(p + "fc2.b")), st);
+    for (size_t i = 0; i < sl.size(); ++i) {
+      if (split && l == 0 && i == 1) HIP_OK(hipStreamWaitEvent(e->st2, e->ev_mid, 0));
+      decoder_layer(e, sl[i], l, row_pos, row_hyp, done, lin, align_map, n_align, attn, cross_group,
+                    (split && l == 0 && i == 0) ? e->ev_mid : nullptr);
     }
   }
-  {
-    ProfScope ps(e, P_DEC_OTHER, st);
-    launch_layernorm(x, d, logit_rows, n_logit, d, e->Wf("dec.ln.w"), e->Wf("dec.ln.b"), hb, d, st);
+  for (const auto& s : sl) {
+    const int nl = split ? s.rows : n_logit;
+    const int* lr = split ? nullptr : logit_rows;
+    {
+      ProfScope ps(e, P_DEC_OTHER, s.st);
+      launch_layernorm(e->s_x.as<float>() + (size_t)s.r0 * d, d, lr, nl, d, e->Wf("dec.ln.w"), e->Wf("dec.ln.b"),
+                       e->s_hb.as<bf16>() + (size_t)s.r0 * d, d, s.st);
+    }
+    const size_t wsb = 64ull << 20;
+    s.ws->ensure(wsb);
+    ProfScope ps(e, P_LOGITS_GEMM, s.st, 2.0 * nl * m.n_vocab * d, gemm_bytes(nl, m.n_vocab, d, 4));
+    launch_gemm(amat(e->s_hb.as<bf16>() + (size_t)s.r0 * d, d), e->Wb("dec.embed"), d, nl, m.n_vocab, d,
+                epi_of(EPI_F32, logits + (size_t)s.r0 * m.n_vocab, m.n_vocab, nullptr), s.ws->as<float>(), wsb, s.st);
   }
-  gemm_p(e, P_LOGITS_GEMM, amat(hb, d), e->Wb("dec.embed"), d, n_logit, m.n_vocab, d, epi_of(EPI_F32, logits, m.n_vocab, nullptr), st);
+  if (split) {
+    HIP_OK(hipEventRecord(e->ev_join, e->st2));
+    HIP_OK(hipStreamWaitEvent(st, e->ev_join, 0));
+  }
 }
 
 void check_weights(wm_engine* e) {
@@ -624,7 +724,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     }
     // logits rows of a decode step are the hypotheses themselves
     decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                 e->d_lin.as<int>(), e->d_row_hyp.as<int>(), NH, logits, nullptr, 0, nullptr, per, st);
+                 e->d_lin.as<int>(), nullptr, NH, logits, nullptr, 0, nullptr, per, st);
     select(step);
     ++steps;
   }
@@ -812,6 +912,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     auto* e = new wm_engine();
     e->dm = *dims;
     e->device = device;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     try {
       build_layout(e);
       build_frontend(e, nullptr);
@@ -837,8 +938,11 @@ void wm_destroy(wm_engine* e) {
                     &e->d_row_pos, &e->d_row_hyp, &e->d_hyp_slot, &e->d_n_active, &e->d_suppress, &e->d_cand_tok,
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
-                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->prof_dbytes})
+                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes})
     b->release();
+  if (e->st2) (void)hipStreamDestroy(e->st2);
+  for (hipEvent_t ev : {e->ev_fork, e->ev_mid, e->ev_join})
+    if (ev) (void)hipEventDestroy(ev);
   delete e;
 }
 
@@ -961,6 +1065,15 @@ int wm_align(wm_engine* e, int32_t slot, int32_t sot_len, const int32_t* h_sot, 
 int wm_dtw(wm_engine* e, const float* d_cost, int32_t n, int32_t m, int32_t* h_text_idx, int32_t* h_time_idx,
            int32_t* h_path_len, void* stream) {
   return guarded(e, [&] { dtw_run(e, d_cost, n, m, h_text_idx, h_time_idx, h_path_len, (hipStream_t)stream); });
+}
+
+int wm_set_option(wm_engine* e, const char* key, int64_t value) {
+  return guarded(e, [&] {
+    if (!key) throw std::runtime_error("wm_set_option: null key");
+    const std::string k(key);
+    if (k == "decode_split") e->dec_split = value != 0;
+    else throw std::runtime_error("wm_set_option: unknown option " + k);
+  });
 }
 
 int32_t wm_profile_classes(void) { return P_N; }

@@ -47,3 +47,9 @@ void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int
 // Large-M path (gemm_big.hip): 256x128 tiles, LDS-DMA ring; used by launch_gemm when applicable.
 bool gemm_big_applicable(int M, int N, int K);
 void launch_gemm_big(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st);
+
+// Decoder-row path (gemm_dec.hip): M <= 160, N % 64 == 0, every load of a block's K range (KR, a multiple of
+// 64) issued up front; split-K slabs combined by launch_splitk_combine.  Returns false if unsupported.
+bool launch_dec_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     size_t ws_bytes, int KR, hipStream_t st);
+void launch_splitk_combine(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st);

@@ -307,6 +307,24 @@ static void launch_resid_ln_reduce(const float* part, int splitk, int M, int N, 
   WM_LAUNCH_CHECK("resid_ln_reduce_kernel");
 }
 
+// Deterministic combine of `splitk` partial slabs [splitk][M][N] + the epilogue (used by gemm_dec.hip).
+void launch_splitk_combine(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st) {
+  if (epi.kind == EPI_RESID_LN) {
+    launch_resid_ln_reduce(part, splitk, M, N, epi, st);
+    return;
+  }
+  const long long total = (long long)M * N;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+  switch (epi.kind) {
+    case EPI_BF16: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_BF16>), dim3(blocks), dim3(256), 0, st, part, splitk, M, N, epi); break;
+    case EPI_RESID_F32: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_RESID_F32>), dim3(blocks), dim3(256), 0, st, part, splitk, M, N, epi); break;
+    case EPI_F32: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_F32>), dim3(blocks), dim3(256), 0, st, part, splitk, M, N, epi); break;
+    case EPI_DEC_QKV: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_DEC_QKV>), dim3(blocks), dim3(256), 0, st, part, splitk, M, N, epi); break;
+    default: throw std::runtime_error("splitk_combine: bad epilogue kind");
+  }
+  WM_LAUNCH_CHECK("splitk_reduce_kernel");
+}
+
 // Skinny-path geometry: split K so the grid reaches ~256 blocks, each split at least 128 deep (partial
 // slabs cost 8 B per output per split); returns false when the slabs do not fit the scratch.
 static bool skinny_plan(int M, int N, int K, size_t ws_bytes, int* splitk, int* kr) {

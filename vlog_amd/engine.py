@@ -156,6 +156,10 @@ class GpuEngine:
             out[self.lib.wm_profile_name(c).decode()] = dict(launches=n.value, ms=ms.value, flops=fl.value, bytes=by.value)
         return out
 
+    def set_option(self, key: str, value: int) -> None:
+        """Engine scheduling knob (wm_set_option), e.g. set_option("decode_split", 0)."""
+        _capi.check(self.lib.wm_set_option(self.h, key.encode(), int(value)), "wm_set_option")
+
     def device_bytes(self) -> int:
         return int(self.lib.wm_device_bytes(self.h))
 
