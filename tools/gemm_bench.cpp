@@ -46,6 +46,8 @@ int main(int argc, char** argv) {
       {"enc.fc2  (16 win)", 24000, 1280, 5120, EPI_RESID_F32},
       {"enc.out  (16 win)", 24000, 1280, 1280, EPI_RESID_F32},
       {"cross-kv (16 win)", 24000, 81920, 1280, EPI_BF16},
+      {"tiny.qkv (16 win)", 24000, 1152, 384, EPI_BF16},
+      {"tiny.fc2 (ragged)", 3001, 384, 1536, EPI_RESID_F32},
       {"dec.qkv  (150 rows)", 150, 3840, 1280, EPI_BF16},
       {"dec.fc1  (150 rows)", 150, 5120, 1280, EPI_BF16},
       {"dec.fc2  (150 rows)", 150, 1280, 5120, EPI_RESID_F32},

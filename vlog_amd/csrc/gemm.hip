@@ -440,6 +440,10 @@ void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int
     const char* e = std::getenv("VLOG_AMD_GEMM_BIG");
     return !(e && e[0] == '0');
   }();
+  static const bool p8_enabled = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_8P");
+    return !(e && e[0] == '0');
+  }();
   static const bool skinny_enabled = [] {
     const char* e = std::getenv("VLOG_AMD_GEMM_SKINNY");
     return !(e && e[0] == '0');
@@ -453,6 +457,10 @@ void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int
     return;
   }
   const bool vec4 = epi.ldc % 4 == 0 && (epi.rpb == 0 || epi.bstride % 4 == 0);   // 4-column vector epilogue
+  if (p8_enabled && vec4 && gemm_8p_applicable(M, N, K)) {
+    launch_gemm_8p(a, w, ldw, M, N, K, epi, st);
+    return;
+  }
   if (big_enabled && vec4 && gemm_big_applicable(M, N, K)) {
     launch_gemm_big(a, w, ldw, M, N, K, epi, st);
     return;

@@ -1,0 +1,203 @@
+// Large-M bf16 GEMM for gfx950 (encoder projections/MLP, conv stem, cross-KV projection): C = A . W^T, both
+// operands K-contiguous.  256 x 256 output tile per 512-thread block, 8 waves as 2 (M) x 4 (N), each wave
+// 128 x 64 = 8 x 4 fragments of v_mfma_f32_16x16x32_bf16 (operands swapped: the W fragment is the MFMA A
+// operand, so a lane's accumulator holds 4 consecutive output columns of one row -> vector epilogue).
+//
+// Schedule (cdna_hip_programming.md §5 "The 256² 8-phase template", restated for this layout):
+//  * BK = 64 K-tiles, LDS double buffer: [2][A 256 x 64 | W 256 x 64] bf16 = 128 KiB in ONE __shared__ array.
+//    Rows are 128 B; 16-B chunk c of row r sits in slot c ^ ((r >> 1) & 7) (applied to the LDS-DMA source
+//    address; the image itself is lane-linear).
+//  * Each K-tile is 4 phases, one per 64 x 32 quadrant of the wave's output (Q00, Q01, Q11, Q10: each step
+//    reloads ONE operand set).  A phase = [ds_read the new operand fragments, issue part of the NEXT tile's
+//    LDS-DMA] lgkmcnt(0) s_barrier [setprio 1, 16 MFMAs, setprio 0] s_barrier.
+//  * The two wave groups (wm = 0 / 1; one wave of each on every SIMD) run one barrier apart: group 1 takes
+//    an extra barrier at entry (group 0 one at exit), so on every SIMD one wave's MFMAs overlap the other
+//    wave's LDS reads and DMA issue.
+//  * Tile t+1 is DMA'd into the other buffer during tile t's phases 0-1 (its last readers retired their
+//    reads with lgkmcnt(0) before the barrier that opened tile t) and waited (vmcnt(0)) in phase 3 before
+//    the barrier that ends that wave's read slot, so every reader of tile t+1 is past a barrier that follows
+//    every issuing wave's wait (RAW), and no DMA targets a buffer a wave may still read (WAR).
+#include "gemm.h"
+#include "gemm_epi.h"
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#define P8_BM 256
+#define P8_BN 256
+#define P8_BK 64
+#define P8_TILE (P8_BM * P8_BK)          // elements of one operand tile (A or W)
+#define P8_BUF (2 * P8_TILE)             // A + W of one K-tile
+
+__device__ __forceinline__ int p8_swz(int row, int ch) { return row * P8_BK + ((ch ^ ((row >> 1) & 7)) << 3); }
+
+// LATE (variant B): LDS reads retire AFTER the slot-ending barrier (their latency overlaps the barrier wait);
+// the next tile's DMA then moves one phase later (phases 1-2) so no DMA can overwrite bytes still in flight
+// to a reader (its reads of the previous tile retire by the barrier after its MFMA slot).
+template <int KIND, bool LATE>
+__global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M,
+                                                         int N, int K, GemmEpi epi, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * P8_BUF];
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = wgid / tiles_n, tn = wgid - tm * tiles_n;
+  const int m0 = tm * P8_BM, n0 = tn * P8_BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // DMA sources.  Quarter qq of a K-tile = A rows [0,128) | A rows [128,256) | W rows [0,128) | W rows [128,256);
+  // wave `wid` moves rows [qq*128 + 16 wid, +16) of each quarter as two 8-row x 128-B wave-instructions.
+  const bf16* src[4][2];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (qq & 1) * 128 + wid * 16 + j * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      if (qq < 2) {
+        int gr = m0 + row;
+        if (gr >= M) gr = M - 1;
+        const long long off = a.rpb ? (long long)(gr / a.rpb) * a.bstride + (long long)(gr % a.rpb) * a.ld : (long long)gr * a.ld;
+        src[qq][j] = a.ptr + off + ch * 8;
+      } else {
+        int gn = n0 + row;
+        if (gn >= N) gn = N - 1;
+        src[qq][j] = w + (long long)gn * ldw + ch * 8;
+      }
+    }
+  auto dma = [&](int qq, int t) {
+    bf16* dst = smem + (t & 1) * P8_BUF + (qq >> 1) * P8_TILE + ((qq & 1) * 128 + wid * 16) * P8_BK;
+    const int k0 = t * P8_BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(src[qq][j] + k0),
+                                       (__attribute__((address_space(3))) void*)(dst + j * 8 * P8_BK), 16, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / P8_BK;
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) dma(qq, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (wm == 1) asm volatile("s_barrier" ::: "memory");   // stagger: group 1 runs one barrier behind
+
+  bf16x8 fa[4][2], fb[2][2];                          // [frag][k-step]
+  auto read_a = [&](const bf16* sA, int half) {       // wave rows wm*128 + half*64 + 16 i
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        fa[i][kk] = *(const bf16x8*)(sA + p8_swz(wm * 128 + half * 64 + i * 16 + fr, kk * 4 + fq));
+  };
+  auto read_b = [&](const bf16* sB, int half) {       // wave cols wn*64 + half*32 + 16 j
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        fb[j][kk] = *(const bf16x8*)(sB + p8_swz(wn * 64 + half * 32 + j * 16 + fr, kk * 4 + fq));
+  };
+  auto mfma_q = [&](int ha, int hb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ha * 4 + i][hb * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // end of a read slot: this wave's LDS reads retired, then the barrier; MFMAs stay below it
+#define P8_READ_DONE()                                                          \
+  if (LATE) {                                                                   \
+    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");          \
+  } else {                                                                      \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");          \
+  }                                                                             \
+  __builtin_amdgcn_sched_barrier(0);
+#define P8_MFMA_DONE()                                          \
+  __builtin_amdgcn_sched_barrier(0);                            \
+  asm volatile("s_barrier" ::: "memory");
+
+  for (int t = 0; t < nk; ++t) {
+    const bf16* sA = smem + (t & 1) * P8_BUF;
+    const bf16* sB = sA + P8_TILE;
+    const bool more = t + 1 < nk;
+    // phase 0: Q00 (A half 0, W half 0) + DMA quarters 0, 1 of tile t+1
+    read_b(sB, 0);
+    read_a(sA, 0);
+    if (!LATE && more) { dma(0, t + 1); dma(1, t + 1); }
+    P8_READ_DONE();
+    mfma_q(0, 0);
+    P8_MFMA_DONE();
+    // phase 1: Q01 (W half 1) + DMA quarters 2, 3
+    read_b(sB, 1);
+    if (more) { dma(2, t + 1); dma(3, t + 1); }
+    P8_READ_DONE();
+    mfma_q(0, 1);
+    P8_MFMA_DONE();
+    // phase 2: Q11 (A half 1)
+    read_a(sA, 1);
+    if (LATE && more) { dma(0, t + 1); dma(1, t + 1); }
+    P8_READ_DONE();
+    mfma_q(1, 1);
+    P8_MFMA_DONE();
+    // phase 3: Q10 (W half 0); tile t+1 has landed (this wave's share) before this read slot ends
+    read_b(sB, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    P8_READ_DONE();
+    mfma_q(1, 0);
+    P8_MFMA_DONE();
+  }
+  if (wm == 0) asm volatile("s_barrier" ::: "memory");   // balance the stagger
+#undef P8_READ_DONE
+#undef P8_MFMA_DONE
+
+  // acc[i][j] holds C^T: lane l has row m = m0 + wm*128 + 16 i + (l & 15), columns n = ... + 4 (l >> 4) + e
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wm * 128 + i * 16 + fr;
+    if (row >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col0 = n0 + wn * 64 + j * 16 + 4 * fq;
+      if (col0 < N) apply_epi4<KIND>(epi, row, col0, acc[i][j]);
+    }
+  }
+}
+
+template <int KIND>
+static void run_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st) {
+  static const bool late = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_8P");
+    return e && e[0] == '2';
+  }();
+  const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
+  if (late)
+    hipLaunchKernelGGL((gemm_8p_kernel<KIND, true>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_8p_kernel<KIND, false>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
+  WM_LAUNCH_CHECK("gemm_8p_kernel");
+}
+
+bool gemm_8p_applicable(int M, int N, int K) { return M >= 1024 && N >= 256 && N % 4 == 0 && K % P8_BK == 0 && K >= P8_BK; }
+
+void launch_gemm_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st) {
+  switch (epi.kind) {
+    case EPI_BF16: run_8p<EPI_BF16>(a, w, ldw, M, N, K, epi, st); break;
+    case EPI_RESID_F32: run_8p<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, st); break;
+    case EPI_GELU_POS_F32: run_8p<EPI_GELU_POS_F32>(a, w, ldw, M, N, K, epi, st); break;
+    case EPI_F32: run_8p<EPI_F32>(a, w, ldw, M, N, K, epi, st); break;
+    case EPI_DEC_QKV: run_8p<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, st); break;
+    case EPI_CROSS_KV: run_8p<EPI_CROSS_KV>(a, w, ldw, M, N, K, epi, st); break;
+    default: throw std::runtime_error("launch_gemm_8p: bad epilogue kind");
+  }
+}
