@@ -124,6 +124,10 @@ int wm_align(wm_engine* e, int32_t slot, int32_t sot_len, const int32_t* h_sot, 
 int wm_dtw(wm_engine* e, const float* d_cost, int32_t n, int32_t m, int32_t* h_text_idx, int32_t* h_time_idx,
            int32_t* h_path_len, void* stream);
 
+/* Encoder self-attention kernel alone (diagnostics / parity tests; wm_encode runs it per layer):
+ * d_qkv bf16 [B][T][3 n_state] (q | k | v, head h at columns h*64), d_out bf16 [B][T][n_state]. */
+int wm_encoder_attention(wm_engine* e, const void* d_qkv, void* d_out, int32_t B, int32_t T, void* stream);
+
 /* Bytes of device memory held by the engine (weights + caches + scratch). */
 int64_t wm_device_bytes(wm_engine* e);
 
@@ -139,7 +143,10 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_split" (default 0): decode steps with >= 32 rows run as two row slices on two streams, one
  *   slice's weight GEMMs overlapping the other's cross-attention.  Results are bit-identical
  *   either way; off by default because the overlap measured slower on MI355X (the GEMM blocks queue behind
- *   the cross-attention blocks). */
+ *   the cross-attention blocks).
+ *   "decode_ring_gemm" (default 0): decoder projections with K <= 1280 use the ring-pipelined GEMM (one
+ *   pass over K, no split-K slabs) instead of the split-K skinny GEMM; faster in isolation, measured
+ *   slower inside the decode step on MI355X, so off by default. */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);
 /* As wm_profile(e, 1) but only the classes whose bit is set in class_mask are timed (0 disables), so a
  * timed run can keep events on the dominant kernel alone. */

@@ -10,7 +10,7 @@ import os
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwhisper_mi355.so")
+LIB_PATH = os.environ.get("VLOG_AMD_LIB") or os.path.join(_HERE, "libwhisper_mi355.so")
 ABI_VERSION = 1
 
 # Every entry point include/whisper_mi355.h declares (tests check the library exports all of them).
@@ -18,7 +18,7 @@ SYMBOLS = (
     "wm_create", "wm_destroy", "wm_last_error", "wm_abi_version", "wm_set_weight", "wm_weights_complete",
     "wm_logmel", "wm_logmel_finalize", "wm_encode", "wm_reserve", "wm_cross_kv", "wm_generate", "wm_forward",
     "wm_frame_energy", "wm_align", "wm_dtw", "wm_device_bytes", "wm_profile_classes", "wm_profile_name", "wm_profile", "wm_profile_select",
-    "wm_profile_read", "wm_set_option",
+    "wm_profile_read", "wm_set_option", "wm_encoder_attention",
 )
 
 
@@ -78,6 +78,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "wm_profile": (C.c_int, [vp, i32]),
         "wm_profile_select": (C.c_int, [vp, C.c_uint32]),
         "wm_set_option": (C.c_int, [vp, C.c_char_p, i64]),
+        "wm_encoder_attention": (C.c_int, [vp, vp, vp, i32, i32, vp]),
         "wm_profile_read": (C.c_int, [vp, i32, C.POINTER(i64), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),
     }

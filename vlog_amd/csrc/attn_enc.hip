@@ -12,6 +12,7 @@
 // A-operand reads are two ds_read_b64 per lane.  Next tile's global loads are issued before the current
 // tile's MFMAs (register double buffer).
 #include "common.h"
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -160,11 +161,200 @@ __global__ __launch_bounds__(256) void attn_enc_kernel(const bf16* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------------------
+// v2: 32x32x16 MFMA flash attention, one wave = 32 queries, 4 waves = 128 queries of one (window, head).
+//   S^T (32 keys x 32 queries) = K . Q^T with Q pre-scaled by scale*log2(e) (bf16) held as the B operand,
+//   K row fragments (ds_read_b128) as the A operand -> lane (q = l&31, h = l>>5) holds 16 scores of query
+//   q, keys 8g + 4h + e (g, e < 4): the row max is 16 in-lane max + one xor-32 shuffle, the row sum stays
+//   lane-local until the end.
+//   O^T (32 hd x 32 q) += V^T . P^T: the S^T accumulator converted pairwise to bf16 IS the B operand
+//   (k-step s takes registers 8s..8s+7 = keys 16s + 8(j>>2) + 4h + (j&3)); the V^T A operand comes from
+//   row-major V in LDS through ds_read_b64_tr_b16 (cdna_hip_programming.md §3, T10), two reads per k-step.
+//   Online softmax with deferred rescale (T13, THR = 8 in log2 units: P <= 256, exact in the normalised
+//   result); K/V register-staged one tile ahead (T14) into a double-buffered LDS image, one barrier/tile.
+//   LDS images (128-B rows): K chunk c of row r at slot c ^ ((r >> 1) & 7) (conflict-free 32-row b128
+//   reads); V chunk c of row r at slot c ^ (((r >> 1) & 1) << 2) (conflict-free 4-row tr_b16 reads).
+#define A2_KT 64
+#define A2_THR 8.0f
+typedef __attribute__((ext_vector_type(4))) short i16x4;
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+
+__device__ __forceinline__ int a2_kslot(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 7)) << 3); }
+__device__ __forceinline__ int a2_vslot(int r, int c) { return r * 64 + ((c ^ (((r >> 1) & 1) << 2)) << 3); }
+
+__global__ __launch_bounds__(256, 2) void attn_enc_v2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                             int T, int d, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * A2_KT * HD];     // [buf][K | V][64 keys][64]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ql = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const long long ld = 3LL * d;
+  const bf16* base = qkv + (long long)b * T * ld + h * HD;
+  const int q = blockIdx.x * 128 + wv * 32 + ql;
+
+  // Q (B operand of S^T): k-step s holds Q[q][16 s + 8 hh + j], pre-scaled
+  bf16x8 qf[4];
+  {
+    const int qc = min(q, T - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 v = *(const bf16x8*)(base + (long long)qc * ld + 16 * s + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(bf2f(v[j]) * scale_log2);
+    }
+  }
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  // staging: thread moves 16-B chunks (row = c >> 3, chunk = c & 7) for c = tid, tid + 256 of K and of V
+  i32x4 rk[2], rv[2];
+  const int nt = (T + A2_KT - 1) / A2_KT;
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * 256, key = min(t * A2_KT + (c >> 3), T - 1), ch = c & 7;
+      const bf16* p = base + (long long)key * ld + ch * 8;
+      rk[i] = *(const i32x4*)(p + d);
+      rv[i] = *(const i32x4*)(p + 2 * d);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    bf16* sK = smem + buf * (2 * A2_KT * HD);
+    bf16* sV = sK + A2_KT * HD;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * 256, r = c >> 3, ch = c & 7;
+      *(i32x4*)(sK + a2_kslot(r, ch)) = rk[i];
+      *(i32x4*)(sV + a2_vslot(r, ch)) = rv[i];
+    }
+  };
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  const int G = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;    // tr_b16: group, row q, col block p
+  for (int t = 0; t < nt; ++t) {
+    const bf16* sK = smem + (t & 1) * (2 * A2_KT * HD);
+    const bf16* sV = sK + A2_KT * HD;
+    if (t + 1 < nt) load_tile(t + 1);
+
+    // ---- S^T for the two 32-key blocks
+    f32x16 sc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 ka = *(const bf16x8*)(sK + a2_kslot(kb * 32 + ql, 2 * s + hh));
+        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sc[kb], 0, 0, 0);
+      }
+    }
+    if (t == nt - 1) {                                   // keys past T (last tile only)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = t * A2_KT + kb * 32 + 8 * (r >> 2) + 4 * hh + (r & 3);
+          if (key >= T) sc[kb][r] = -INFINITY;
+        }
+    }
+    // ---- online softmax, deferred rescale
+    float mx = sc[0][0];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (__any(mx > m_run + A2_THR)) {
+      const float mn = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      m_run = mn;
+    }
+    bf16x8 pf[2][2];                                    // [key block][k-step]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(sc[kb][r] - m_run);
+        l_run += pv;
+        pf[kb][r >> 3][r & 7] = f2bf(pv);
+      }
+    // ---- O^T += V^T . P^T
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+          bf16x8 va;
+#ifndef A2_SCALAR_V
+          i32x2 vw[2];
+#endif
+#pragma unroll
+          for (int jh = 0; jh < 2; ++jh) {
+            const int row = kb * 32 + 16 * s + 8 * jh + 4 * (G >> 1) + gq;
+            const int col = 32 * hb + 16 * (G & 1) + 4 * gp;             // hd element
+#ifdef A2_SCALAR_V
+            const int rowb = row - gq, hdc = 32 * hb + 16 * (G & 1) + gi;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) va[4 * jh + e] = sV[a2_vslot(rowb + e, hdc >> 3) + (hdc & 7)];
+#else
+            const bf16* ad = sV + a2_vslot(row, col >> 3) + (col & 7);
+            // (whole-register bit casts: an element-wise short -> bf16 insert here miscompiles on ROCm 7.2,
+            //  duplicating one half of the fragment)
+            vw[jh] = __builtin_bit_cast(i32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                   (__attribute__((address_space(3))) i16x4*)(ad)));
+#endif
+          }
+#ifndef A2_SCALAR_V
+          va = __builtin_bit_cast(bf16x8, i32x4{vw[0][0], vw[0][1], vw[1][0], vw[1][1]});
+#endif
+          o[hb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[kb][s], o[hb], 0, 0, 0);
+        }
+    if (t + 1 < nt) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (q < T) {
+    const float inv = 1.0f / l_run;
+    bf16* orow = out + ((long long)b * T + q) * d + h * HD;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[hb][4 * g + e] * inv);
+        *(bf16x4*)(orow + 32 * hb + 8 * g + 4 * hh) = w;
+      }
+  }
+}
+
 void launch_attn_enc(const bf16* qkv, bf16* out, int B, int T, int d, int n_head, hipStream_t st) {
   if (B <= 0) return;
   if (d != n_head * HD) throw std::runtime_error("attn_enc: head_dim must be 64");
-  dim3 grid((T + 63) / 64, n_head, B);
+  static const bool v1 = [] {
+    const char* e = std::getenv("VLOG_AMD_ATTN_V1");
+    return e && e[0] == '1';
+  }();
   const float scale_log2 = 0.125f * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_enc_kernel, grid, dim3(256), 0, st, qkv, out, T, d, scale_log2);
+  if (v1) {
+    dim3 grid((T + 63) / 64, n_head, B);
+    hipLaunchKernelGGL(attn_enc_kernel, grid, dim3(256), 0, st, qkv, out, T, d, scale_log2);
+  } else {
+    dim3 grid((T + 127) / 128, n_head, B);
+    hipLaunchKernelGGL(attn_enc_v2_kernel, grid, dim3(256), 0, st, qkv, out, T, d, scale_log2);
+  }
   WM_LAUNCH_CHECK("attn_enc_kernel");
 }

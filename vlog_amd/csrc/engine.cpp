@@ -125,6 +125,7 @@ struct wm_engine {
   double prof_flops[P_N] = {0}, prof_bytes[P_N] = {0};
   DevBuf gemm_ws, gemm_ws2;  // split-K partial slabs (per decoder slice stream)
   // two-slice decode (decoder_pass): second stream + fork/phase/join events
+  bool dec_ring = false;     // ring-pipelined decoder GEMMs for K <= 1280 (gemm_dec.hip): r01 in situ slower than skinny
   bool dec_split = false;   // measured slower on MI355X (r01: GEMMs queue behind cross-attention blocks)
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
@@ -443,7 +444,10 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   auto gemm = [&](const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
     const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : 2;
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
-    launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
+    // K <= 1280: the ring-pipelined decoder GEMM (no split-K); wider K (fc2) keeps the split-K skinny path.
+    // The choice follows the whole pass's rows (sl.total_rows) so slicing never changes a row's arithmetic.
+    if (!(e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st)))
+      launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
   };
   // residual-producing GEMMs also apply the LayerNorm that consumes the residual (EPI_RESID_LN: fused into
   // the split-K combine on the skinny path): out -> ln2, cout -> ln3, fc2 -> next layer's ln1
@@ -913,6 +917,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     e->dm = *dims;
     e->device = device;
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
     try {
       build_layout(e);
       build_frontend(e, nullptr);
@@ -1067,11 +1072,19 @@ int wm_dtw(wm_engine* e, const float* d_cost, int32_t n, int32_t m, int32_t* h_t
   return guarded(e, [&] { dtw_run(e, d_cost, n, m, h_text_idx, h_time_idx, h_path_len, (hipStream_t)stream); });
 }
 
+int wm_encoder_attention(wm_engine* e, const void* d_qkv, void* d_out, int32_t B, int32_t T, void* stream) {
+  return guarded(e, [&] {
+    if (B <= 0 || T <= 0) throw std::runtime_error("wm_encoder_attention: bad B/T");
+    launch_attn_enc((const bf16*)d_qkv, (bf16*)d_out, B, T, e->dm.n_state, e->dm.n_head, (hipStream_t)stream);
+  });
+}
+
 int wm_set_option(wm_engine* e, const char* key, int64_t value) {
   return guarded(e, [&] {
     if (!key) throw std::runtime_error("wm_set_option: null key");
     const std::string k(key);
     if (k == "decode_split") e->dec_split = value != 0;
+    else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }

@@ -57,3 +57,6 @@ void launch_gemm_big(const GemmA& a, const bf16* w, long long ldw, int M, int N,
 bool launch_dec_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      size_t ws_bytes, int KR, hipStream_t st);
 void launch_splitk_combine(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st);
+// Ring-pipelined decoder-row path (gemm_dec.hip): M <= 160; kr = K range per block (0 = whole K up to 1280).
+bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     size_t ws_bytes, int kr, hipStream_t st);

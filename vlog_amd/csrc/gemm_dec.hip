@@ -160,6 +160,149 @@ bool launch_dec_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   return true;
 }
 
+// ------------------------------------------------------------------------------------------------------
+// Ring-pipelined decoder GEMM: one block = 32 output columns x all rows (MF fragments of 16, MF even) x a
+// K range of kr (the whole K when the activations are <= 1280 wide: no split-K, no partial slabs, no
+// combine launch).  A-row panels and W-row panels of 64 k (128-B rows, XOR-swizzled chunks on the DMA
+// source) stream through an R-slot LDS ring by LDS-DMA, R-1 panels in flight; every wave waits for its own
+// DMAs of panel p with a counted vmcnt, and the raw barrier after it both publishes panel p to all waves and
+// frees the slot of panel p-1 (whose readers' ds_reads retired before their MFMAs) for panel p+R-1.
+// Waves: 2 (16 columns each) x 2 (row halves of MF/2 fragments).
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+#define VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    VMW(0) VMW(1) VMW(2) VMW(3) VMW(4) VMW(5) VMW(6) VMW(7) VMW(8) VMW(9) VMW(10) VMW(11) VMW(12) VMW(13)
+    VMW(14) VMW(15) VMW(16) VMW(17) VMW(18) VMW(19) VMW(20) VMW(21) VMW(22) VMW(23) VMW(24) VMW(25) VMW(26)
+    VMW(27) VMW(28) VMW(29) VMW(30) VMW(31) VMW(32) VMW(33) VMW(34) VMW(35) VMW(36)
+#undef VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int MF, int KIND, int R>
+__global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
+                                                       int K, GemmEpi epi, int tiles_n, int splitk, int kr,
+                                                       float* __restrict__ part) {
+  static_assert(MF % 2 == 0, "MF must be even");
+  constexpr int ROWS = MF * 16, HALF = MF / 2, SLOT = (ROWS + 32) * 64, DA = ROWS / 32, DPP = DA + 1;
+  __shared__ __attribute__((aligned(16))) bf16 smem[R * SLOT];
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int split = wgid % splitk, tile = wgid / splitk;
+  const int n0 = tile * 32;
+  const int kb = split * kr, klen = min(kr, K - kb), NP = klen / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid & 1, wr = wid >> 1;
+
+  // DMA sources: wave `wid` moves A rows [wid*ROWS/4, +ROWS/4) (DA instructions of 8 rows) and W rows [8 wid, +8)
+  const bf16* srcA[DA];
+#pragma unroll
+  for (int j = 0; j < DA; ++j) {
+    const int row = wid * (ROWS / 4) + j * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    const int gr = min(row, M - 1);
+    const long long off = a.rpb ? (long long)(gr / a.rpb) * a.bstride + (long long)(gr % a.rpb) * a.ld : (long long)gr * a.ld;
+    srcA[j] = a.ptr + off + kb + ch * 8;
+  }
+  const bf16* srcW;
+  {
+    const int row = wid * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    srcW = w + (long long)min(n0 + row, N - 1) * ldw + kb + ch * 8;
+  }
+  auto issue = [&](int p) {
+    bf16* s = smem + (p % R) * SLOT;
+#pragma unroll
+    for (int j = 0; j < DA; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + p * 64),
+                                       (__attribute__((address_space(3))) void*)(s + (wid * (ROWS / 4) + j * 8) * 64), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(srcW + p * 64),
+                                     (__attribute__((address_space(3))) void*)(s + (ROWS + wid * 8) * 64), 16, 0, 0);
+  };
+
+  f32x4 acc[HALF];
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int pre = min(R - 1, NP);
+  for (int p = 0; p < pre; ++p) issue(p);
+  for (int p = 0; p < NP; ++p) {
+    vm_wait(min(NP - 1 - p, R - 2) * DPP);            // this wave's DMAs of panel p have landed
+    asm volatile("s_barrier" ::: "memory");           // ... everyone's; slot of panel p-1 is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (p + R - 1 < NP) issue(p + R - 1);
+    const bf16* sA = smem + (p % R) * SLOT;
+    const bf16* sW = sA + ROWS * 64;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + (lane >> 4);
+      const bf16x8 fb = *(const bf16x8*)(sW + dswz(wc * 16 + (lane & 15), ch));
+      bf16x8 fa[HALF];
+#pragma unroll
+      for (int i = 0; i < HALF; ++i) fa[i] = *(const bf16x8*)(sA + dswz((wr * HALF + i) * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < HALF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[i], 0, 0, 0);
+    }
+  }
+
+  const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
+  const int col0 = n0 + wc * 16 + 4 * (lane >> 4);
+  if (col0 >= N) return;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const int row = (wr * HALF + i) * 16 + (lane & 15);
+    if (row >= M) continue;
+    if (to_slab)
+      *(f32x4*)(part + ((long long)split * M + row) * N + col0) = acc[i];
+    else
+      apply_epi4<KIND>(epi, row, col0, acc[i]);
+  }
+}
+
+template <int MF, int KIND>
+static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     int splitk, int kr, hipStream_t st) {
+  constexpr int R = MF <= 4 ? 8 : MF <= 8 ? 7 : 6;     // (MF*16 + 32) * 128 B per slot, <= 144 KiB in all
+  const int tiles_n = (N + 31) / 32;
+  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R>), dim3(tiles_n * splitk), dim3(256), 0, st, a, w, ldw, M, N, K, epi,
+                     tiles_n, splitk, kr, ws);
+  WM_LAUNCH_CHECK("dec_ring_kernel");
+}
+
+template <int KIND>
+static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
+                          float* ws, int splitk, int kr, hipStream_t st) {
+  if (M <= 32) run_ring<2, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 64) run_ring<4, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 96) run_ring<6, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (M <= 128) run_ring<8, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_ring<10, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+}
+
+// Ring path: M <= 160, N % 4 == 0, K % 64 == 0.  kr = K range per block (0: the whole K up to 1280, else split
+// into ceil(K / 1280) ranges).  Returns false when unsupported.
+bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     size_t ws_bytes, int kr, hipStream_t st) {
+  if (M > 160 || N % 4 != 0 || K % 64 != 0) return false;
+  if (kr <= 0) kr = K <= 1280 ? K : ((K + (K + 1279) / 1280 - 1) / ((K + 1279) / 1280) + 63) / 64 * 64;
+  if (kr % 64 != 0) return false;
+  const int splitk = (K + kr - 1) / kr;
+  if ((K - (splitk - 1) * kr) % 64 != 0) return false;
+  const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
+  if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
+  if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
+  switch (epi.kind) {
+    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    default: return false;
+  }
+  if (slab) launch_splitk_combine(ws, splitk, M, N, epi, st);
+  return true;
+}
+
 // microbenchmark entry (tools/dec_gemm_bench): the GEMM body alone (no combine), with ablation bits
 void launch_dec_gemm_body(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, float* ws, int KR, int abl,
                           hipStream_t st) {

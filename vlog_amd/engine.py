@@ -156,6 +156,16 @@ class GpuEngine:
             out[self.lib.wm_profile_name(c).decode()] = dict(launches=n.value, ms=ms.value, flops=fl.value, bytes=by.value)
         return out
 
+    def encoder_attention(self, qkv: torch.Tensor) -> torch.Tensor:
+        """The encoder self-attention kernel alone: qkv bf16 [B, T, 3d] -> bf16 [B, T, d] (diagnostics/tests)."""
+        B, T, three_d = qkv.shape
+        if qkv.dtype != torch.bfloat16 or three_d != 3 * self.dims.n_state or not qkv.is_contiguous():
+            raise ValueError("encoder_attention: qkv must be contiguous bf16 [B, T, 3 n_state]")
+        out = torch.empty(B, T, self.dims.n_state, dtype=torch.bfloat16, device=self.device)
+        _capi.check(self.lib.wm_encoder_attention(self.h, C.c_void_p(qkv.data_ptr()), C.c_void_p(out.data_ptr()),
+                                                  B, T, self.stream_ptr()), "wm_encoder_attention")
+        return out
+
     def set_option(self, key: str, value: int) -> None:
         """Engine scheduling knob (wm_set_option), e.g. set_option("decode_split", 0)."""
         _capi.check(self.lib.wm_set_option(self.h, key.encode(), int(value)), "wm_set_option")
