@@ -11,6 +11,9 @@
 #include <vector>
 #include "../vlog_amd/csrc/gemm.h"
 
+void launch_gemm_8p_abl(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, int abl,
+                        hipStream_t st);
+
 #define CK(x)                                                                        \
   do {                                                                               \
     hipError_t e_ = (x);                                                             \
@@ -113,6 +116,30 @@ int main(int argc, char** argv) {
     const double gbs = 2.0 * ((double)s.M * s.K + (double)s.N * s.K) / (us * 1e-6) / 1e9;
     std::printf("%-20s M=%6d N=%6d K=%5d  %10.1f us  %7.1f TF/s  %7.1f GB/s(A+W)  max rel err %.2e %s\n", s.name, s.M,
                 s.N, s.K, us, tf, gbs, maxerr, maxerr < 2e-2 ? "ok" : "BAD");
+  }
+  // ablations of the 8-phase encoder GEMM on the qkv / fc1 shapes (bit 0: no epilogue, 1: no MFMA, 2: no DMA)
+  if (std::getenv("GEMM_ABL")) {
+    for (auto& s : shapes) {
+      if (s.M < 1024 || s.kind != EPI_BF16 || s.N > 8192) continue;
+      GemmEpi ep;
+      std::memset(&ep, 0, sizeof(ep));
+      ep.kind = EPI_BF16;
+      ep.out = dC;
+      ep.ldc = s.N;
+      GemmA a{dA, (long long)s.K, 0, 0};
+      for (int abl : {0, 1, 2, 3, 4, 5, 7}) {
+        launch_gemm_8p_abl(a, dW, s.K, s.M, s.N, s.K, ep, abl, st);
+        CK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; ++r) launch_gemm_8p_abl(a, dW, s.K, s.M, s.N, s.K, ep, abl, st);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = 1000.0 * ms / reps;
+        std::printf("%-20s 8p abl=%d (skip%s%s%s)  %9.1f us  %7.1f TF/s\n", s.name, abl, (abl & 1) ? " epi" : "",
+                    (abl & 2) ? " mfma" : "", (abl & 4) ? " dma" : "", us, 2.0 * s.M * s.N * s.K / (us * 1e-6) / 1e12);
+      }
+    }
   }
   return 0;
 }

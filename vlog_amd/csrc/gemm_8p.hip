@@ -28,16 +28,20 @@
 #define P8_BK 64
 #define P8_TILE (P8_BM * P8_BK)          // elements of one operand tile (A or W)
 #define P8_BUF (2 * P8_TILE)             // A + W of one K-tile
+#define P8_SR16 (P8_BN + 16)             // staged bf16 epilogue: LDS row stride (elements)
+#define P8_SR32 (P8_BN + 4)              // staged f32 epilogue (128-row halves): LDS row stride (floats)
+#define P8_SMEM (P8_BM * P8_SR16 > 2 * P8_BUF ? P8_BM * P8_SR16 : 2 * P8_BUF)   // bf16 elements
 
 __device__ __forceinline__ int p8_swz(int row, int ch) { return row * P8_BK + ((ch ^ ((row >> 1) & 7)) << 3); }
 
-// LATE (variant B): LDS reads retire AFTER the slot-ending barrier (their latency overlaps the barrier wait);
-// the next tile's DMA then moves one phase later (phases 1-2) so no DMA can overwrite bytes still in flight
-// to a reader (its reads of the previous tile retire by the barrier after its MFMA slot).
-template <int KIND, bool LATE>
+// ABL (microbenchmark ablations only; the product uses 0): bit 0 skips the epilogue stores, bit 1 the MFMAs,
+// bit 2 the LDS-DMA of tiles 1.. (the LDS keeps tile 0), each skipped part's inputs kept live.
+// (A variant that retired the LDS reads after the slot barrier, with the DMA one phase later, measured
+// 2-8 % slower on the encoder shapes and was dropped.)
+template <int KIND, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M,
                                                          int N, int K, GemmEpi epi, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * P8_BUF];
+  __shared__ __attribute__((aligned(16))) bf16 smem[P8_SMEM];
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -68,6 +72,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
       }
     }
   auto dma = [&](int qq, int t) {
+    if ((ABL & 4) && t > 0) return;
     bf16* dst = smem + (t & 1) * P8_BUF + (qq >> 1) * P8_TILE + ((qq & 1) * 128 + wid * 16) * P8_BK;
     const int k0 = t * P8_BK;
 #pragma unroll
@@ -104,6 +109,16 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
         fb[j][kk] = *(const bf16x8*)(sB + p8_swz(wn * 64 + half * 32 + j * 16 + fr, kk * 4 + fq));
   };
   auto mfma_q = [&](int ha, int hb) {
+    if (ABL & 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" :: "v"(fa[i][kk]));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" :: "v"(fb[j][kk]));
+      }
+      return;
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -116,12 +131,8 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
     __builtin_amdgcn_s_setprio(0);
   };
   // end of a read slot: this wave's LDS reads retired, then the barrier; MFMAs stay below it
-#define P8_READ_DONE()                                                          \
-  if (LATE) {                                                                   \
-    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");          \
-  } else {                                                                      \
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");          \
-  }                                                                             \
+#define P8_READ_DONE()                                          \
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
   __builtin_amdgcn_sched_barrier(0);
 #define P8_MFMA_DONE()                                          \
   __builtin_amdgcn_sched_barrier(0);                            \
@@ -134,7 +145,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
     // phase 0: Q00 (A half 0, W half 0) + DMA quarters 0, 1 of tile t+1
     read_b(sB, 0);
     read_a(sA, 0);
-    if (!LATE && more) { dma(0, t + 1); dma(1, t + 1); }
+    if (more) { dma(0, t + 1); dma(1, t + 1); }
     P8_READ_DONE();
     mfma_q(0, 0);
     P8_MFMA_DONE();
@@ -146,7 +157,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
     P8_MFMA_DONE();
     // phase 2: Q11 (A half 1)
     read_a(sA, 1);
-    if (LATE && more) { dma(0, t + 1); dma(1, t + 1); }
     P8_READ_DONE();
     mfma_q(1, 1);
     P8_MFMA_DONE();
@@ -161,7 +171,70 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
 #undef P8_READ_DONE
 #undef P8_MFMA_DONE
 
-  // acc[i][j] holds C^T: lane l has row m = m0 + wm*128 + 16 i + (l & 15), columns n = ... + 4 (l >> 4) + e
+  if (ABL & 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
+    return;
+  }
+  // acc[i][j] holds C^T: lane l has row m = m0 + wm*128 + 16 i + (l & 15), columns n = ... + 4 (l >> 4) + e.
+  // Staged epilogue: the tile goes through LDS (free once the balancing barrier above has passed: every
+  // wave's last reads retired before it, and the last tile issues no DMA) and leaves as whole 512-B (bf16)
+  // or 1-KiB (f32) row segments, 16 B per lane, instead of 16 rows x 8-16 B per store instruction.
+  constexpr bool BF16_OUT = KIND == EPI_BF16 || KIND == EPI_CROSS_KV;
+  constexpr bool F32_OUT = KIND == EPI_RESID_F32 || KIND == EPI_F32 || KIND == EPI_GELU_POS_F32;
+  if (BF16_OUT && N % 8 == 0 && epi.ldc % 8 == 0 && (epi.rpb == 0 || epi.bstride % 8 == 0 || KIND == EPI_CROSS_KV)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rl = wm * 128 + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cl = wn * 64 + j * 16 + 4 * fq;
+        const int col0 = min(n0 + cl, N - 4);
+        const f32x4 v = epi_value4<KIND>(epi, m0 + rl, col0, acc[i][j]);
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        *(bf16x4*)(smem + rl * P8_SR16 + cl) = o;
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int c = tid + 512 * k, rl = c >> 5, cc = (c & 31) * 8;
+      const int row = m0 + rl, col0 = n0 + cc;
+      if (row < M && col0 < N) epi_store8_bf16<KIND>(epi, row, col0, *(const bf16x8*)(smem + rl * P8_SR16 + cc));
+    }
+    return;
+  }
+  if (F32_OUT && epi.ldc % 4 == 0) {
+    float* sf = (float*)smem;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (wm == half) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int rl = i * 16 + fr;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cl = wn * 64 + j * 16 + 4 * fq;
+            const int col0 = min(n0 + cl, N - 4);
+            *(f32x4*)(sf + rl * P8_SR32 + cl) = epi_value4<KIND>(epi, m0 + half * 128 + rl, col0, acc[i][j]);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int k = 0; k < 16; ++k) {
+        const int c = tid + 512 * k, rl = c >> 6, cc = (c & 63) * 4;
+        const int row = m0 + half * 128 + rl, col0 = n0 + cc;
+        if (row < M && col0 < N) epi_store4_f32<KIND>(epi, row, col0, *(const f32x4*)(sf + rl * P8_SR32 + cc));
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = m0 + wm * 128 + i * 16 + fr;
@@ -176,15 +249,8 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
 
 template <int KIND>
 static void run_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st) {
-  static const bool late = [] {
-    const char* e = std::getenv("VLOG_AMD_GEMM_8P");
-    return e && e[0] == '2';
-  }();
   const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
-  if (late)
-    hipLaunchKernelGGL((gemm_8p_kernel<KIND, true>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
-  else
-    hipLaunchKernelGGL((gemm_8p_kernel<KIND, false>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
+  hipLaunchKernelGGL((gemm_8p_kernel<KIND>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
   WM_LAUNCH_CHECK("gemm_8p_kernel");
 }
 
@@ -199,5 +265,22 @@ void launch_gemm_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, 
     case EPI_DEC_QKV: run_8p<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, st); break;
     case EPI_CROSS_KV: run_8p<EPI_CROSS_KV>(a, w, ldw, M, N, K, epi, st); break;
     default: throw std::runtime_error("launch_gemm_8p: bad epilogue kind");
+  }
+}
+
+// microbenchmark entry (tools/gemm_bench): EPI_BF16 body with ablation bits
+void launch_gemm_8p_abl(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, int abl,
+                        hipStream_t st) {
+  const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
+  const dim3 g(tiles_m * tiles_n);
+  switch (abl) {
+    case 0: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 0>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    case 1: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 1>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    case 2: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 2>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    case 3: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 3>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    case 4: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 4>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    case 5: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 5>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    case 7: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 7>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    default: throw std::runtime_error("launch_gemm_8p_abl: bad ablation");
   }
 }

@@ -132,3 +132,50 @@ __device__ __forceinline__ void apply_epi4(const GemmEpi& epi, int row, int col0
       break;
   }
 }
+
+// ---- Staged epilogue helpers (gemm_8p.hip): the value of 4 consecutive outputs (bias / activation /
+// positional add folded in, same arithmetic as apply_epi4), and whole 16-B chunk stores of it.
+template <int KIND>
+__device__ __forceinline__ f32x4 epi_value4(const GemmEpi& epi, int row, int col0, f32x4 acc) {
+  f32x4 v = acc;
+  if (epi.bias) {
+    const f32x4 b = *(const f32x4*)(epi.bias + col0);
+    v += b;
+  }
+  if (KIND == EPI_BF16 && epi.act == 1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+  }
+  if (KIND == EPI_GELU_POS_F32) {
+    const int t = row % epi.rpb;
+    const f32x4 pe = *(const f32x4*)(epi.pos + (long long)t * epi.ldc + col0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) + pe[e];
+  }
+  return v;
+}
+
+// 8 consecutive bf16 outputs (col0 % 8 == 0) of a bf16-output kind
+template <int KIND>
+__device__ __forceinline__ void epi_store8_bf16(const GemmEpi& epi, int row, int col0, bf16x8 v) {
+  if (KIND == EPI_BF16) {
+    const long long o = epi.rpb ? (long long)(row / epi.rpb) * epi.bstride + (long long)(row % epi.rpb + epi.roff) * epi.ldc
+                                : (long long)row * epi.ldc;
+    *(bf16x8*)((bf16*)epi.out + o + col0) = v;
+  } else if (KIND == EPI_CROSS_KV) {
+    const int d = epi.d, hd = epi.head_dim;
+    const int l2 = col0 / d, cc = col0 - l2 * d;
+    const int h = cc / hd, e2 = cc - h * hd;
+    const int b = row / epi.rpb, t = row - b * epi.rpb;
+    const long long o = ((((long long)l2 * epi.n_slots + epi.slot0 + b) * epi.n_head + h) * epi.rpb + t) * hd + e2;
+    *(bf16x8*)((bf16*)epi.out + o) = v;
+  }
+}
+
+// 4 consecutive f32 outputs of an f32-output kind (RESID_F32 adds into the residual)
+template <int KIND>
+__device__ __forceinline__ void epi_store4_f32(const GemmEpi& epi, int row, int col0, f32x4 v) {
+  f32x4* p = (f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0);
+  if (KIND == EPI_RESID_F32) *p = *p + v;
+  else *p = v;
+}
