@@ -144,9 +144,11 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   slice's weight GEMMs overlapping the other's cross-attention.  Results are bit-identical
  *   either way; off by default because the overlap measured slower on MI355X (the GEMM blocks queue behind
  *   the cross-attention blocks).
- *   "decode_ring_gemm" (default 0): decoder projections with K <= 1280 use the ring-pipelined GEMM (one
- *   pass over K, no split-K slabs) instead of the split-K skinny GEMM; faster in isolation, measured
- *   slower inside the decode step on MI355X, so off by default. */
+ *   "decode_ring_gemm" (default 1): the wide decoder projections with K <= 1280 (self-attention QKV, fc1)
+ *   use the ring-pipelined GEMM (one pass over K, no split-K slabs or combine launch); 0 uses the split-K
+ *   skinny GEMM for every decoder projection.
+ *   "cross_attn_blocks" (default 2 per CU): grid cap of the cross-attention kernel, which walks its
+ *   (window, head, key split) items with a grid stride; 0 launches one block per item. */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);
 /* As wm_profile(e, 1) but only the classes whose bit is set in class_mask are timed (0 disables), so a
  * timed run can keep events on the dominant kernel alone. */

@@ -208,14 +208,12 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
 // Per (row, lane group) an online softmax keeps (m, l, o[8]); groups merge by xor-shuffles, waves through
 // LDS.  With splits > 1 the (m, l, o) partials go to cross_combine_kernel (per row, as the legacy path).
 template <int RG>
-__global__ __launch_bounds__(256) void cross_attn_group_kernel(DecAttnArgs a) {
-  __shared__ float s_m[4][RG], s_l[4][RG];
-  __shared__ float s_o[4][RG][HD];
+__device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int split, float (&s_m)[4][RG],
+                                           float (&s_l)[4][RG], float (&s_o)[4][RG][HD]) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int sub = lane & 7, g = lane >> 3;
   const int H = a.H;
-  const int grp = blockIdx.x / H, h = blockIdx.x - grp * H;
-  const int split = blockIdx.y;
+  const int grp = bx / H, h = bx - grp * H;
   const int row0 = grp * RG;
   bool live[RG];
   bool any = false;
@@ -232,7 +230,7 @@ __global__ __launch_bounds__(256) void cross_attn_group_kernel(DecAttnArgs a) {
   const bf16* K = a.kbase + off + sub * 8;
   const bf16* V = a.vbase + off + sub * 8;
   if (a.stat && tid == 0)
-    atomicAdd(a.stat + ((blockIdx.x + blockIdx.y) & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + RG * 2 * HD * 2));
+    atomicAdd(a.stat + ((bx + split) & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + RG * 2 * HD * 2));
 
   float qf[RG][8];
 #pragma unroll
@@ -342,10 +340,25 @@ __global__ __launch_bounds__(256) void cross_attn_group_kernel(DecAttnArgs a) {
   }
 }
 
+// Items (group x head x key split) are walked with a grid stride: launched with one block per item this is
+// the plain grid; launched with a capped grid (persistent form) each block takes every gridDim.x-th item, so
+// the kernel holds a bounded number of wave slots per CU and kernels on other streams (the decoder's weight
+// GEMMs) always find room beside it.
 template <int RG>
-static void launch_group(dim3 grid, const DecAttnArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-  if (ev0) hipExtLaunchKernelGGL(cross_attn_group_kernel<RG>, grid, dim3(256), 0, st, ev0, ev1, 0, a);
-  else hipLaunchKernelGGL(cross_attn_group_kernel<RG>, grid, dim3(256), 0, st, a);
+__global__ __launch_bounds__(256) void cross_attn_group_kernel(DecAttnArgs a, int n_items) {
+  __shared__ float s_m[4][RG], s_l[4][RG];
+  __shared__ float s_o[4][RG][HD];
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    cross_item<RG>(a, it / a.splits, it % a.splits, s_m, s_l, s_o);
+    __syncthreads();
+  }
+}
+
+template <int RG>
+static void launch_group(int n_items, int cap, const DecAttnArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+  const dim3 grid(cap > 0 ? std::min(n_items, cap) : n_items);
+  if (ev0) hipExtLaunchKernelGGL(cross_attn_group_kernel<RG>, grid, dim3(256), 0, st, ev0, ev1, 0, a, n_items);
+  else hipLaunchKernelGGL(cross_attn_group_kernel<RG>, grid, dim3(256), 0, st, a, n_items);
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -473,7 +486,7 @@ void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* 
 void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf16* vbase, int T, const int* hyp_slot,
                        const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H, int group,
                        float* part_m, float* part_l, float* part_o, float* probs, const int* head_map, int n_align,
-                       int plan_rows, unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                       int plan_rows, int cap, unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
   if (plan_rows < rows) plan_rows = rows;
   DecAttnArgs a{};
@@ -502,18 +515,18 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
   int splits = ((rg == 1 ? 10240 : 2048) + plan_blocks - 1) / plan_blocks;
   splits = std::max(1, std::min(splits, std::min(16, T / 128)));
   a.splits = splits;
-  const dim3 grid(blocks, splits);
+  const int n_items = blocks * splits;
   // events (profiler): start on the attention kernel, stop on the last kernel of the pair
   hipEvent_t e0 = ev0, e1 = splits == 1 ? ev1 : nullptr;
   switch (rg) {
-    case 1: launch_group<1>(grid, a, st, e0, e1); break;
-    case 2: launch_group<2>(grid, a, st, e0, e1); break;
-    case 3: launch_group<3>(grid, a, st, e0, e1); break;
-    case 4: launch_group<4>(grid, a, st, e0, e1); break;
-    case 5: launch_group<5>(grid, a, st, e0, e1); break;
-    case 6: launch_group<6>(grid, a, st, e0, e1); break;
-    case 7: launch_group<7>(grid, a, st, e0, e1); break;
-    default: launch_group<8>(grid, a, st, e0, e1); break;
+    case 1: launch_group<1>(n_items, cap, a, st, e0, e1); break;
+    case 2: launch_group<2>(n_items, cap, a, st, e0, e1); break;
+    case 3: launch_group<3>(n_items, cap, a, st, e0, e1); break;
+    case 4: launch_group<4>(n_items, cap, a, st, e0, e1); break;
+    case 5: launch_group<5>(n_items, cap, a, st, e0, e1); break;
+    case 6: launch_group<6>(n_items, cap, a, st, e0, e1); break;
+    case 7: launch_group<7>(n_items, cap, a, st, e0, e1); break;
+    default: launch_group<8>(n_items, cap, a, st, e0, e1); break;
   }
   WM_LAUNCH_CHECK("cross_attn_group_kernel");
   if (splits > 1) {

@@ -37,7 +37,7 @@ void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
 void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const int*, const int*, const int*, const int*,
                       bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
-                       long long, int, int, int, float*, float*, float*, float*, const int*, int, int,
+                       long long, int, int, int, float*, float*, float*, float*, const int*, int, int, int,
                        unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
@@ -125,8 +125,10 @@ struct wm_engine {
   double prof_flops[P_N] = {0}, prof_bytes[P_N] = {0};
   DevBuf gemm_ws, gemm_ws2;  // split-K partial slabs (per decoder slice stream)
   // two-slice decode (decoder_pass): second stream + fork/phase/join events
-  bool dec_ring = false;     // ring-pipelined decoder GEMMs for K <= 1280 (gemm_dec.hip): r01 in situ slower than skinny
-  bool dec_split = false;   // measured slower on MI355X (r01: GEMMs queue behind cross-attention blocks)
+  bool dec_ring = true;      // ring-pipelined decoder GEMMs for the wide K <= 1280 projections (gemm_dec.hip)
+  bool dec_split = false;    // two-stream row slices (see decoder_pass)
+  int cross_cap = -1;        // cross-attention grid cap (0: one block per item; >0: persistent grid-stride
+                             // form; -1: 2 blocks per CU, set at wm_create)
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
   std::vector<DecLayerW> dec_w;
@@ -444,9 +446,13 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   auto gemm = [&](const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
     const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : 2;
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
-    // K <= 1280: the ring-pipelined decoder GEMM (no split-K); wider K (fc2) keeps the split-K skinny path.
-    // The choice follows the whole pass's rows (sl.total_rows) so slicing never changes a row's arithmetic.
-    if (!(e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st)))
+    // Wide projections with K <= 1280 (self-attention QKV, fc1: N >= 3K) take the ring-pipelined GEMM: one
+    // pass over K, epilogue applied in place, no split-K slabs and no combine launch.  The square ones (out,
+    // cq, cout) and fc2 (K = 4d) keep the split-K skinny path, which measured faster for them in the decode
+    // step.  The choice follows the whole pass's rows (sl.total_rows) so slicing never changes a row's
+    // arithmetic.
+    if (!(e->dec_ring && K <= 1280 && N >= 3 * K && sl.total_rows <= 160 &&
+          launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st)))
       launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
   };
   // residual-producing GEMMs also apply the LayerNorm that consumes the residual (EPI_RESID_LN: fused into
@@ -489,7 +495,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
                       e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, cross_group, e->s_pm.as<float>() + po,
                       e->s_pl.as<float>() + po, e->s_po.as<float>() + po * 64, probs, hmap, n_align, sl.total_rows,
-                      e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+                      e->cross_cap, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
   }
   if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
   gemm(amat(ao, d), W.cout_w, d, d, d, resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
@@ -916,8 +922,14 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     auto* e = new wm_engine();
     e->dm = *dims;
     e->device = device;
+    {
+      int n_cu = 0;
+      HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+      e->cross_cap = 2 * std::max(1, n_cu);
+    }
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     try {
       build_layout(e);
       build_frontend(e, nullptr);
@@ -1085,6 +1097,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     const std::string k(key);
     if (k == "decode_split") e->dec_split = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
+    else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }
