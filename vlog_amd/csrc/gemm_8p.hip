@@ -38,7 +38,7 @@ __device__ __forceinline__ int p8_swz(int row, int ch) { return row * P8_BK + ((
 // bit 2 the LDS-DMA of tiles 1.. (the LDS keeps tile 0), each skipped part's inputs kept live.
 // (A variant that retired the LDS reads after the slot barrier, with the DMA one phase later, measured
 // 2-8 % slower on the encoder shapes and was dropped.)
-template <int KIND, int ABL = 0>
+template <int KIND, int ABL = 0, bool EARLY = true>
 __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M,
                                                          int N, int K, GemmEpi epi, int tiles_n) {
   __shared__ __attribute__((aligned(16))) bf16 smem[P8_SMEM];
@@ -90,10 +90,16 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
   const int nk = K / P8_BK;
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) dma(qq, 0);
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (EARLY && nk > 1) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) dma(qq, 1);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   if (wm == 1) asm volatile("s_barrier" ::: "memory");   // stagger: group 1 runs one barrier behind
 
-  bf16x8 fa[4][2], fb[2][2];                          // [frag][k-step]
+  bf16x8 fa[4][2], fb[2][2], fb2[2][2];               // [frag][k-step]; fb2: W half 1 (EARLY schedule)
   auto read_a = [&](const bf16* sA, int half) {       // wave rows wm*128 + half*64 + 16 i
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -101,14 +107,14 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
       for (int kk = 0; kk < 2; ++kk)
         fa[i][kk] = *(const bf16x8*)(sA + p8_swz(wm * 128 + half * 64 + i * 16 + fr, kk * 4 + fq));
   };
-  auto read_b = [&](const bf16* sB, int half) {       // wave cols wn*64 + half*32 + 16 j
+  auto read_b = [&](const bf16* sB, int half, bf16x8 (&dst)[2][2]) {   // wave cols wn*64 + half*32 + 16 j
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        fb[j][kk] = *(const bf16x8*)(sB + p8_swz(wn * 64 + half * 32 + j * 16 + fr, kk * 4 + fq));
+        dst[j][kk] = *(const bf16x8*)(sB + p8_swz(wn * 64 + half * 32 + j * 16 + fr, kk * 4 + fq));
   };
-  auto mfma_q = [&](int ha, int hb) {
+  auto mfma_q = [&](int ha, int hb, const bf16x8 (&fb)[2][2]) {
     if (ABL & 2) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -141,30 +147,62 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
   for (int t = 0; t < nk; ++t) {
     const bf16* sA = smem + (t & 1) * P8_BUF;
     const bf16* sB = sA + P8_TILE;
+    if (EARLY) {
+      // Both W halves stay in registers (fb, fb2), so W is read in phases 0-1 and A in phases 0 and 2:
+      // the W region of this buffer is free from phase 2 and the A region from phase 3, and tile t+2 is
+      // DMA'd into them there (its readers are >= 4 phases away).  The wait in phase 3 leaves exactly those
+      // 8 DMAs in flight and retires tile t+1's (issued in phases 2-3 of tile t-1).
+      const bool more2 = t + 2 < nk;
+      read_b(sB, 0, fb);                                // phase 0: Q00
+      read_a(sA, 0);
+      P8_READ_DONE();
+      mfma_q(0, 0, fb);
+      P8_MFMA_DONE();
+      read_b(sB, 1, fb2);                               // phase 1: Q01
+      P8_READ_DONE();
+      mfma_q(0, 1, fb2);
+      P8_MFMA_DONE();
+      read_a(sA, 1);                                    // phase 2: Q11 + W of tile t+2
+      if (more2) { dma(2, t + 2); dma(3, t + 2); }
+      P8_READ_DONE();
+      mfma_q(1, 1, fb2);
+      P8_MFMA_DONE();
+      if (more2) {                                      // phase 3: Q10 + A of tile t+2
+        dma(0, t + 2);
+        dma(1, t + 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      P8_READ_DONE();
+      mfma_q(1, 0, fb);
+      P8_MFMA_DONE();
+      continue;
+    }
     const bool more = t + 1 < nk;
     // phase 0: Q00 (A half 0, W half 0) + DMA quarters 0, 1 of tile t+1
-    read_b(sB, 0);
+    read_b(sB, 0, fb);
     read_a(sA, 0);
     if (more) { dma(0, t + 1); dma(1, t + 1); }
     P8_READ_DONE();
-    mfma_q(0, 0);
+    mfma_q(0, 0, fb);
     P8_MFMA_DONE();
     // phase 1: Q01 (W half 1) + DMA quarters 2, 3
-    read_b(sB, 1);
+    read_b(sB, 1, fb);
     if (more) { dma(2, t + 1); dma(3, t + 1); }
     P8_READ_DONE();
-    mfma_q(0, 1);
+    mfma_q(0, 1, fb);
     P8_MFMA_DONE();
     // phase 2: Q11 (A half 1)
     read_a(sA, 1);
     P8_READ_DONE();
-    mfma_q(1, 1);
+    mfma_q(1, 1, fb);
     P8_MFMA_DONE();
     // phase 3: Q10 (W half 0); tile t+1 has landed (this wave's share) before this read slot ends
-    read_b(sB, 0);
+    read_b(sB, 0, fb);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     P8_READ_DONE();
-    mfma_q(1, 0);
+    mfma_q(1, 0, fb);
     P8_MFMA_DONE();
   }
   if (wm == 0) asm volatile("s_barrier" ::: "memory");   // balance the stagger
@@ -249,8 +287,15 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
 
 template <int KIND>
 static void run_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st) {
+  static const bool early = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_8P");
+    return !(e && e[0] == '2');
+  }();
   const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
-  hipLaunchKernelGGL((gemm_8p_kernel<KIND>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
+  if (early)
+    hipLaunchKernelGGL((gemm_8p_kernel<KIND, 0, true>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_8p_kernel<KIND, 0, false>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
   WM_LAUNCH_CHECK("gemm_8p_kernel");
 }
 
