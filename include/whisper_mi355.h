@@ -147,8 +147,11 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_ring_gemm" (default 1): the wide decoder projections with K <= 1280 (self-attention QKV, fc1)
  *   use the ring-pipelined GEMM (one pass over K, no split-K slabs or combine launch); 0 uses the split-K
  *   skinny GEMM for every decoder projection.
- *   "cross_attn_blocks" (default 2 per CU): grid cap of the cross-attention kernel, which walks its
- *   (window, head, key split) items with a grid stride; 0 launches one block per item. */
+ *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its
+ *   (window, head, key split) items with a grid stride; 0 launches one block per item.
+ *   "cross_attn_fuse" (default 1): bit 0 folds the cq projection's split-K combine into the cross-attention
+ *   kernel's q load; bit 1 combines the key splits in-kernel (last-arriving split) instead of a combine
+ *   launch.  Every setting of these three knobs gives bit-identical results. */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);
 /* As wm_profile(e, 1) but only the classes whose bit is set in class_mask are timed (0 disables), so a
  * timed run can keep events on the dominant kernel alone. */

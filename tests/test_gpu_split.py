@@ -1,6 +1,7 @@
-"""Two-slice decode (decoder rows split over two streams so one slice's weight GEMMs overlap the
-other's cross-attention) must give bit-identical results to the one-stream pass: same tokens, same scores,
-same no-speech probabilities, for greedy and beam search.  Runs through the C-ABI on the MI355X."""
+"""Scheduling knobs must not change results: the two-slice decode (decoder rows split over two streams), the
+fused cross-attention (cq split-K combine + key-split combine folded into the attention kernel) and its
+persistent grid form give bit-identical tokens, scores and no-speech probabilities to the plain schedule,
+for greedy and beam search.  Runs through the C-ABI on the MI355X."""
 import numpy as np
 import pytest
 import torch
@@ -29,14 +30,37 @@ def batch():
     return dims, eng
 
 
-def _run(eng, dims, split, **kw):
+def _run(eng, dims, split, opts=(), **kw):
     st = dims.specials
     eng.set_option("decode_split", split)
+    for k, v in opts:
+        eng.set_option(k, v)
     prompt = [st.sot, st.lang_token("en"), st.transcribe]
     sup = [st.transcribe, st.translate, st.sot, st.sot_prev, st.sot_lm]
     res, steps = eng.generate(list(range(W)), [prompt] * W, suppress_tokens=sup, max_length=120, **kw)
-    eng.set_option("decode_split", 0)
+    eng.set_option("decode_split", 0)                 # back to the defaults
+    eng.set_option("cross_attn_fuse", 1)
+    eng.set_option("cross_attn_blocks", 0)
     return res, steps
+
+
+def _same(a, sa, b, sb):
+    assert sa == sb
+    for ra, rb in zip(a, b):
+        assert ra.tokens == rb.tokens
+        assert ra.score == rb.score and ra.cum_logprob == rb.cum_logprob
+        assert ra.no_speech_prob == rb.no_speech_prob
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0)], ids=["greedy", "beam5"])
+@pytest.mark.parametrize("opts", [(("cross_attn_fuse", 0),), (("cross_attn_blocks", 512),),
+                                  (("cross_attn_fuse", 3), ("cross_attn_blocks", 512))],
+                         ids=["unfused", "persistent", "combine-fused-persistent"])
+def test_cross_attention_forms_bit_identical(batch, kw, opts):
+    dims, eng = batch
+    a, sa = _run(eng, dims, 0, **kw)
+    b, sb = _run(eng, dims, 0, opts=opts, **kw)
+    _same(a, sa, b, sb)
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0)], ids=["greedy", "beam5"])

@@ -42,6 +42,12 @@ struct DecAttnArgs {
   float* probs; const int* head_map; int n_align;
   float scale_log2;
   unsigned long long* stat;   // profiler byte counter: STAT_SLOTS slots, summed on read (no hot atomic)
+  // cross, fused forms: (1) q = bf16(sum of q_splits split-K slabs [s][q_rows][ldq] + q_bias) instead of
+  // reading a.q (the cq projection's combine folded in, same summation order as splitk_reduce_kernel);
+  // (2) key splits combined in-kernel by the last-arriving split of each (group, head), counted in cnt
+  // (zero between launches: the last arriver resets its word).
+  const float* q_part; int q_splits, q_rows; const float* q_bias;
+  int* cnt;
 };
 
 #define CT_MAX 1536
@@ -235,7 +241,20 @@ __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int spl
   float qf[RG][8];
 #pragma unroll
   for (int r = 0; r < RG; ++r) {
-    load8(a.q + (long long)(row0 + r) * a.ldq + h * HD + sub * 8, qf[r]);
+    if (a.q_part) {
+      const long long slab = (long long)a.q_rows * a.ldq;
+      const float* pq = a.q_part + (long long)(row0 + r) * a.ldq + h * HD + sub * 8;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < a.q_splits; ++sp) {
+        const f32x4 lo = *(const f32x4*)(pq + sp * slab), hi = *(const f32x4*)(pq + sp * slab + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { v[i] += lo[i]; v[4 + i] += hi[i]; }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qf[r][i] = bf2f(f2bf(v[i] + a.q_bias[h * HD + sub * 8 + i]));
+    } else {
+      load8(a.q + (long long)(row0 + r) * a.ldq + h * HD + sub * 8, qf[r]);
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) qf[r][i] *= a.scale_log2;
   }
@@ -332,10 +351,51 @@ __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int spl
     const int row = row0 + r;
     if (a.splits == 1) {
       if (!(a.done && a.done[a.row_hyp[row]])) a.out[(long long)row * a.ldo + h * HD + e] = f2bf(O / L);
+    } else if (a.cnt) {
+      // hand-off to the last-arriving split: write-through (sc1) stores of the partial, drained, then one
+      // agent-scope ticket per item (cdna_hip_programming.md §6 Guideline 16, R1 / counter form)
+      const long long pi = ((long long)row * H + h) * a.splits + split;
+      __hip_atomic_store(a.part_o + pi * HD + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (e == 0) {
+        __hip_atomic_store(a.part_m + pi, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.part_l + pi, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else {
       const long long pi = ((long long)row * H + h) * a.splits + split;
       a.part_o[pi * HD + e] = O;
       if (e == 0) { a.part_m[pi] = M; a.part_l[pi] = L; }
+    }
+  }
+  if (a.splits > 1 && a.cnt) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave's partial has left
+    __syncthreads();
+    if (tid == 0) {
+      int* c = a.cnt + bx;
+      const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == a.splits - 1;
+      if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (s_last) {
+      // same arithmetic and order as cross_combine_kernel; every load of the partials is an sc1 load
+      for (int idx = tid; idx < RG * HD; idx += 256) {
+        const int r = idx / HD, e = idx - r * HD;
+        const int row = row0 + r;
+        if (a.done && a.done[a.row_hyp[row]]) continue;
+        const long long pb = ((long long)row * H + h) * a.splits;
+        float M = -INFINITY;
+        for (int sp = 0; sp < a.splits; ++sp)
+          M = fmaxf(M, __hip_atomic_load(a.part_m + pb + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        float L = 0.f, O = 0.f;
+        for (int sp = 0; sp < a.splits; ++sp) {
+          const float w = exp2f(__hip_atomic_load(a.part_m + pb + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - M);
+          L += __hip_atomic_load(a.part_l + pb + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * w;
+          O += __hip_atomic_load(a.part_o + (pb + sp) * HD + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * w;
+        }
+        a.out[(long long)row * a.ldo + h * HD + e] = f2bf(O / L);
+      }
     }
   }
 }
@@ -486,16 +546,19 @@ void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* 
 void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf16* vbase, int T, const int* hyp_slot,
                        const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H, int group,
                        float* part_m, float* part_l, float* part_o, float* probs, const int* head_map, int n_align,
-                       int plan_rows, int cap, unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                       int plan_rows, int cap, const CrossFuse& fz, unsigned long long* stat, hipStream_t st,
+                       hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
   if (plan_rows < rows) plan_rows = rows;
   DecAttnArgs a{};
+  a.q_part = fz.q_part; a.q_splits = fz.q_splits; a.q_rows = fz.q_rows; a.q_bias = fz.q_bias; a.cnt = fz.cnt;
   a.q = q; a.ldq = ldq; a.kbase = kbase; a.vbase = vbase; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
   a.out = out; a.ldo = ldo; a.H = H; a.T = T; a.n_ctx = T;
   a.part_m = part_m; a.part_l = part_l; a.part_o = part_o; a.probs = probs; a.head_map = head_map; a.n_align = n_align;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;
   if (probs) {        // attention capture (word alignment): the two-pass kernel keeps the probabilities
     if (T > CT_MAX) throw std::runtime_error("cross_attn: too many keys for capture");
+    if (fz.q_part) throw std::runtime_error("cross_attn: fused q slabs unsupported with capture");
     a.splits = 1;
     launch_k(false, dim3(rows * H, 1), a, st, ev0, ev1);
     WM_LAUNCH_CHECK("dec_attn_kernel<cross>");
@@ -517,7 +580,7 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
   a.splits = splits;
   const int n_items = blocks * splits;
   // events (profiler): start on the attention kernel, stop on the last kernel of the pair
-  hipEvent_t e0 = ev0, e1 = splits == 1 ? ev1 : nullptr;
+  hipEvent_t e0 = ev0, e1 = (splits == 1 || fz.cnt) ? ev1 : nullptr;
   switch (rg) {
     case 1: launch_group<1>(n_items, cap, a, st, e0, e1); break;
     case 2: launch_group<2>(n_items, cap, a, st, e0, e1); break;
@@ -529,7 +592,7 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
     default: launch_group<8>(n_items, cap, a, st, e0, e1); break;
   }
   WM_LAUNCH_CHECK("cross_attn_group_kernel");
-  if (splits > 1) {
+  if (splits > 1 && !fz.cnt) {
     if (ev1)
       hipExtLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, nullptr, ev1, 0, part_m, part_l,
                             part_o, row_hyp, done, out, ldo, H, splits);

@@ -40,6 +40,15 @@ __device__ __forceinline__ float ordered_to_float(unsigned int u) {
   return __uint_as_float(u);
 }
 
+// Cross-attention fusions (attn_dec.hip launch_cross_attn): read q as bf16(sum of split-K slabs + bias) and/or
+// combine the key splits in-kernel (last arriver per item, counter words zero between launches).
+struct CrossFuse {
+  const float* q_part = nullptr;   // [q_splits][q_rows][ldq] f32 slabs of the cq projection (nullptr: read q)
+  int q_splits = 0, q_rows = 0;
+  const float* q_bias = nullptr;
+  int* cnt = nullptr;              // >= rows*H zeroed ints (nullptr: separate combine kernel)
+};
+
 // Launch check used by every host-side launcher: converts an asynchronous launch failure into an
 // exception the C-ABI layer turns into an error code + wm_last_error() text.
 #define WM_LAUNCH_CHECK(what)                                                                  \

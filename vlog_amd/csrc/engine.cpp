@@ -38,7 +38,7 @@ void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const in
                       bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
                        long long, int, int, int, float*, float*, float*, float*, const int*, int, int, int,
-                       unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
+                       const CrossFuse&, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
@@ -127,8 +127,11 @@ struct wm_engine {
   // two-slice decode (decoder_pass): second stream + fork/phase/join events
   bool dec_ring = true;      // ring-pipelined decoder GEMMs for the wide K <= 1280 projections (gemm_dec.hip)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
-  int cross_cap = -1;        // cross-attention grid cap (0: one block per item; >0: persistent grid-stride
-                             // form; -1: 2 blocks per CU, set at wm_create)
+  int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
+                             // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
+  DevBuf d_cross_cnt;        // its per-(row, head) arrival counters (zeroed at allocation, reset in-kernel)
+  int cross_cap = 0;         // cross-attention grid cap (0: one block per item; >0: persistent grid-stride form,
+                             // 2 blocks/CU measured ~2 % faster alone but slower with the fused q combine)
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
   std::vector<DecLayerW> dec_w;
@@ -388,6 +391,10 @@ void ensure_step(wm_engine* e, int rows, int logit_rows) {
   e->s_pm.ensure((size_t)rows * H * 16 * 4);
   e->s_pl.ensure((size_t)rows * H * 16 * 4);
   e->s_po.ensure((size_t)rows * H * 16 * 64 * 4);
+  if (e->d_cross_cnt.bytes < (size_t)rows * H * 4) {
+    e->d_cross_cnt.ensure((size_t)rows * H * 4);
+    HIP_OK(hipMemset(e->d_cross_cnt.p, 0, e->d_cross_cnt.bytes));
+  }
   e->d_prow_tok.ensure((size_t)rows * 4);
   e->d_prow_pos.ensure((size_t)rows * 4);
   e->d_prow_hyp.ensure((size_t)rows * 4);
@@ -475,7 +482,19 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
   }
   gemm(amat(ao, d), W.out_w, d, d, d, resid_ln(W.ln2_w, W.ln2_b, W.out_b));
-  gemm(amat(hb, d), W.cq_w, d, d, d, epi_of(EPI_BF16, q, d, W.cq_b));
+  // cq: when the skinny split-K path runs it and no attention is captured, its slabs stay in the scratch and
+  // the cross-attention kernel sums them while loading q (no combine launch)
+  CrossFuse fz;
+  {
+    GemmEpi ep = epi_of(EPI_BF16, q, d, W.cq_b);
+    const int sk = skinny_splits(rows, d, d, wsb);
+    if ((e->cross_fuse & 1) && !(attn && align_map) && sk > 1) {
+      ep.defer_combine = 1;
+      fz.q_part = ws; fz.q_splits = sk; fz.q_rows = rows; fz.q_bias = W.cq_b;
+    }
+    gemm(amat(hb, d), W.cq_w, d, d, d, ep);
+  }
+  if (e->cross_fuse & 2) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   float* probs = nullptr;
   const int* hmap = nullptr;
   if (attn && align_map) {
@@ -495,7 +514,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
                       e->d_hyp_slot.as<int>(), row_hyp, done, ao, d, rows, H, cross_group, e->s_pm.as<float>() + po,
                       e->s_pl.as<float>() + po, e->s_po.as<float>() + po * 64, probs, hmap, n_align, sl.total_rows,
-                      e->cross_cap, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+                      e->cross_cap, fz, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
   }
   if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
   gemm(amat(ao, d), W.cout_w, d, d, d, resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
@@ -922,14 +941,10 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     auto* e = new wm_engine();
     e->dm = *dims;
     e->device = device;
-    {
-      int n_cu = 0;
-      HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-      e->cross_cap = 2 * std::max(1, n_cu);
-    }
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     try {
       build_layout(e);
       build_frontend(e, nullptr);
@@ -955,7 +970,7 @@ void wm_destroy(wm_engine* e) {
                     &e->d_row_pos, &e->d_row_hyp, &e->d_hyp_slot, &e->d_n_active, &e->d_suppress, &e->d_cand_tok,
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
-                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes})
+                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt})
     b->release();
   if (e->st2) (void)hipStreamDestroy(e->st2);
   for (hipEvent_t ev : {e->ev_fork, e->ev_mid, e->ev_join})
@@ -1098,6 +1113,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     if (k == "decode_split") e->dec_split = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
+    else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }

@@ -38,7 +38,13 @@ struct GemmEpi {
   int n_slots, slot0;
   // EPI_RESID_LN: the LayerNorm that consumes the updated residual
   const float* ln_g; const float* ln_b; bf16* ln_out; long long ln_ld;
+  // skinny split-K path only: leave the partial slabs in the scratch (no combine launch) for a consumer
+  // that sums them itself (see skinny_splits)
+  int defer_combine;
 };
+
+// Split count the skinny path would use for this shape (>= 1), or 0 when launch_gemm would not take it.
+int skinny_splits(int M, int N, int K, size_t ws_bytes);
 
 // ws: f32 scratch for split-K partial slabs (nullptr disables split-K)
 void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,

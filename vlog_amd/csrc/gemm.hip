@@ -352,7 +352,7 @@ static void run_skinny(const GemmA& a, const bf16* w, long long ldw, int M, int 
   WM_LAUNCH_CHECK("skinny_kernel");
   if (KIND == EPI_RESID_LN) {
     launch_resid_ln_reduce(ws, splitk, M, N, epi, st);
-  } else if (splitk > 1) {
+  } else if (splitk > 1 && !epi.defer_combine) {
     const long long total = (long long)M * N;
     int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
     hipLaunchKernelGGL((splitk_reduce_kernel<KIND>), dim3(blocks), dim3(256), 0, st, ws, splitk, M, N, epi);
@@ -371,6 +371,16 @@ static void dispatch_skinny(const GemmA& a, const bf16* w, long long ldw, int M,
   else if (M <= 256) run_skinny<16, 128, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
   else if (M <= 320) run_skinny<20, 128, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
   else run_skinny<32, 64, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+}
+
+int skinny_splits(int M, int N, int K, size_t ws_bytes) {
+  static const bool skinny_enabled = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_SKINNY");
+    return !(e && e[0] == '0');
+  }();
+  int splitk, kr;
+  if (!skinny_enabled || M <= 0 || M > 512 || K % BK != 0 || !skinny_plan(M, N, K, ws_bytes, &splitk, &kr)) return 0;
+  return splitk;
 }
 
 static bool try_skinny(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
