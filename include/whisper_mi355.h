@@ -151,7 +151,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   (window, head, key split) items with a grid stride; 0 launches one block per item.
  *   "cross_attn_fuse" (default 1): bit 0 folds the cq projection's split-K combine into the cross-attention
  *   kernel's q load; bit 1 combines the key splits in-kernel (last-arriving split) instead of a combine
- *   launch.  Every setting of these three knobs gives bit-identical results. */
+ *   launch.  Every setting of these three knobs gives bit-identical results.
+ *   "encode_chunk" (default 160): windows per encoder pass inside wm_encode (~52 MB of activation scratch
+ *   per large-v3 window). */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);
 /* As wm_profile(e, 1) but only the classes whose bit is set in class_mask are timed (0 disables), so a
  * timed run can keep events on the dominant kernel alone. */

@@ -303,6 +303,9 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   return true;
 }
 
+// (A register-streaming variant — every wave loading its own fragments from L2/HBM, no LDS — measured 2x
+// slower than the ring on these shapes: ~30-35 GB/s per CU either way, the A re-reads dominate.)
+
 // microbenchmark entry (tools/dec_gemm_bench): the GEMM body alone (no combine), with ablation bits
 void launch_dec_gemm_body(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, float* ws, int KR, int abl,
                           hipStream_t st) {
