@@ -754,8 +754,10 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
       if (act <= 0) break;
     }
     // logits rows of a decode step are the hypotheses themselves
+    // greedy / sampling never reorder hypotheses: the lineage table is the identity and self-attention
+    // reads each row's own cache directly (no dependent lineage load per key block)
     decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                 e->d_lin.as<int>(), nullptr, NH, logits, nullptr, 0, nullptr, per, st);
+                 beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, st);
     select(step);
     ++steps;
   }

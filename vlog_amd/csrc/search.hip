@@ -93,24 +93,33 @@ __device__ float block_sum(float v, float* sh) {
   return r;
 }
 
+// MODE = p.mode as a template parameter (0 greedy, 1 beam top-k, 2 sampling): each instantiation only holds
+// the registers its mode needs next to the register-resident row.
+template <int MODE>
 __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   __shared__ Cand sh_c[NW];
   __shared__ float sh_f[NW];
   __shared__ int s_info[4];
   __shared__ Cand s_top[2][NW * KMAX];
+  __shared__ int s_last_ts;
   const int h = blockIdx.x, tid = threadIdx.x;
   if (p.done[h]) return;
   const int len = p.seq_len[h];
   const int* seq = p.tokens + (long long)h * p.n_ctx;
   const int tb = p.ts_begin;
+  // position of the last sampled timestamp: a block-wide max instead of a serial backward scan (a text-only
+  // history made thread 0 walk the whole sequence one dependent load at a time)
+  if (tid == 0) s_last_ts = -1;
+  __syncthreads();
+  for (int i = p.sample_begin + tid; i < len; i += SB)
+    if (seq[i] >= tb) atomicMax(&s_last_ts, i);
+  __syncthreads();
   if (tid == 0) {
     const int ns = len - p.sample_begin;
     const int last = ns >= 1 ? seq[len - 1] : -1;
     const int last_ts = ns >= 1 && last >= tb;
     const int pen_ts = ns < 2 || seq[len - 2] >= tb;
-    int lastv = -1;
-    for (int i = len - 1; i >= p.sample_begin; --i)
-      if (seq[i] >= tb) { lastv = seq[i]; break; }
+    const int lastv = s_last_ts >= 0 ? seq[s_last_ts] : -1;
     int bound = tb;                          // timestamps in [tb, bound) are masked
     if (lastv >= 0) bound = (last_ts && !pen_ts) ? lastv : lastv + 1;
     s_info[0] = ns == 0;
@@ -137,24 +146,48 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
     }
     return false;
   };
+  // The row is loaded ONCE into registers (PER values per thread, every load issued before any is used),
+  // masked entries recorded in a bitmask; both passes then run on registers.  (The earlier form looped
+  // over the row twice with one dependent global load per iteration: ~90 us per launch of exposed latency.)
+  // Beam (MODE 1) keeps two local top-k lists as well, which with the row would spill: it re-reads the
+  // (L2-resident) row in each pass instead.
+  constexpr int PER = (53248 + SB - 1) / SB;               // vocab <= 53248
+  constexpr bool RES = MODE != 1;
+  float xv[RES ? PER : 1];
+  unsigned long long live = 0;
+  auto xat = [&](int k) -> float { return RES ? xv[k] : lg[tid + k * SB]; };
+  if (RES) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * SB;
+      xv[RES ? k : 0] = i < V ? lg[i] : -INFINITY;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = tid + k * SB;
+    if (i < V && !masked(i)) live |= 1ull << k;
+  }
   // pass 1: per-segment max / argmax (and Gumbel keys for sampling, local top-k for beam)
   Cand mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
   Cand gt{-INFINITY, 0x7fffffff}, gs{-INFINITY, 0x7fffffff};
   Cand kt[KMAX], ks[KMAX];
-  const int K = p.mode == 1 ? p.topk : 0;
+  const int K = MODE == 1 ? p.topk : 0;
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) { kt[j] = Cand{-INFINITY, 0x7fffffff}; ks[j] = kt[j]; }
-  for (int i = tid; i < V; i += SB) {
-    if (masked(i)) continue;
-    const float x = lg[i];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (!((live >> k) & 1)) continue;
+    const int i = tid + k * SB;
+    const float x = xat(k);
     const bool is_ts = i >= tb;
     Cand& m = is_ts ? ms : mt;
     if (better(x, i, m.v, m.i)) { m.v = x; m.i = i; }
-    if (p.mode == 2) {
+    if (MODE == 2) {
       const float key = x * p.inv_temperature + gumbel(p.seed, h, p.step, i);
       Cand& gg = is_ts ? gs : gt;
       if (better(key, i, gg.v, gg.i)) { gg.v = key; gg.i = i; }
-    } else if (K) {
+    } else if (MODE == 1) {
       if (is_ts) topk_insert(ks, K, x, i);
       else topk_insert(kt, K, x, i);
     }
@@ -163,11 +196,12 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   ms = block_argmax(ms, sh_c);
   // pass 2: sum-exp per segment
   float st = 0.f, ss = 0.f;
-  for (int i = tid; i < V; i += SB) {
-    if (masked(i)) continue;
-    const float x = lg[i];
-    if (i >= tb) ss += expf(x - ms.v);
-    else st += expf(x - mt.v);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (!((live >> k) & 1)) continue;
+    const int i = tid + k * SB;
+    if (i >= tb) ss += expf(xat(k) - ms.v);
+    else st += expf(xat(k) - mt.v);
   }
   st = block_sum(st, sh_f);
   ss = block_sum(ss, sh_f);
@@ -180,7 +214,7 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   else if (lse_s == -INFINITY) Z = lse_t;
   else Z = fmaxf(lse_t, lse_s) + log1pf(expf(-fabsf(lse_t - lse_s)));
 
-  if (p.mode == 1) {
+  if (MODE == 1) {
     // merge local top-k lists: wave-level extraction, then thread 0 merges the per-wave winners
     const int wv = tid >> 6;
     wave_topk(kt, K, &s_top[0][wv * KMAX]);
@@ -214,13 +248,13 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
     return;
   }
 
-  if (p.mode == 2) {
+  if (MODE == 2) {
     gt = block_argmax(gt, sh_c);
     gs = block_argmax(gs, sh_c);
   }
   if (tid == 0) {
     int tok;
-    if (p.mode == 2) tok = forced ? gs.i : (better(gt.v, gt.i, gs.v, gs.i) ? gt.i : gs.i);
+    if (MODE == 2) tok = forced ? gs.i : (better(gt.v, gt.i, gs.v, gs.i) ? gt.i : gs.i);
     else tok = forced ? ms.i : (better(mt.v, mt.i, ms.v, ms.i) ? mt.i : ms.i);
     const float lp = lg[tok] - Z;
     p.cum[h] += lp;
@@ -243,8 +277,13 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
 
 void launch_logits_select(const SearchParams& p, int n_hyp, hipStream_t st) {
   if (n_hyp <= 0) return;
+  if (p.V > 53248) throw std::runtime_error("logits_select: vocabulary larger than 53248");
   if (p.mode == 1 && (p.topk < 1 || p.topk > KMAX)) throw std::runtime_error("beam size must be <= 8");
-  hipLaunchKernelGGL(logits_select_kernel, dim3(n_hyp), dim3(SB), 0, st, p);
+  switch (p.mode) {
+    case 0: hipLaunchKernelGGL(logits_select_kernel<0>, dim3(n_hyp), dim3(SB), 0, st, p); break;
+    case 1: hipLaunchKernelGGL(logits_select_kernel<1>, dim3(n_hyp), dim3(SB), 0, st, p); break;
+    default: hipLaunchKernelGGL(logits_select_kernel<2>, dim3(n_hyp), dim3(SB), 0, st, p); break;
+  }
   WM_LAUNCH_CHECK("logits_select_kernel");
 }
 
