@@ -1,0 +1,132 @@
+"""Factored cross-attention (attention over the encoder output, csrc/attn_xenc.hip; the engine default) against
+the projected cross-KV path (csrc/attn_dec.hip, `cross_mode` 0) and the f32 oracle, through the C-ABI.
+
+The two forms are the same arithmetic reassociated (q.(E Wk^T) = (Wk^T q).E, P (E Wv^T + bv) = (P E) Wv^T + bv),
+so they agree to bf16 rounding noise: teacher-forced logits, alignment-head attention and no-speech
+probabilities within the tolerances below, and the same greedy / beam tokens on (almost) every window.  The
+model sizes cover every kernel instantiation: tiny (4 waves x 96 columns), base (8 x 64), small (8 x 96) and,
+without the oracle, large-v3 (8 x 160, the bench configuration)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import mel as omel
+from oracle.model import OracleWhisper
+from vlog_amd.audio import speech_like
+from vlog_amd.dims import model_dims
+from vlog_amd.weights import round_bf16, synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _sup(st):
+    return [st.transcribe, st.translate, st.sot, st.sot_prev, st.sot_lm]
+
+
+def _engine(name, seed, W, eot_after=40):
+    from vlog_amd.engine import GpuEngine
+    dims = model_dims(name)
+    sd = synthetic_state_dict(dims, seed=seed, eot_after=eot_after)
+    eng = GpuEngine(dims, sd, 0)
+    x = np.concatenate([speech_like(30.0, 900 + seed * 10 + i) for i in range(W)])
+    feats = omel.log_mel(x, dims.n_mels)
+    enc = eng.encode(torch.from_numpy(feats).cuda(), [3000 * i for i in range(W)], [3000] * W)
+    return dims, sd, eng, enc
+
+
+def _both(eng, enc, W, n_hyp, fn):
+    """fn() under the projected (0) and factored (1) cross-attention; the engine is left in factored mode."""
+    out = {}
+    for mode in (0, 1):
+        eng.set_option("cross_mode", mode)
+        eng.reserve(W, n_hyp)
+        eng.cross_kv(enc, 0)
+        out[mode] = fn()
+    return out[0], out[1]
+
+
+@pytest.fixture(scope="module", params=["tiny", "base", "small"])
+def small_models(request):
+    W = 4
+    dims, sd, eng, enc = _engine(request.param, 7, W)
+    orc = OracleWhisper(round_bf16(sd), dims, np.float32)
+    return dims, eng, enc, orc, W
+
+
+def test_factored_logits_match_projected_and_oracle(small_models):
+    dims, eng, enc, orc, W = small_models
+    st = dims.specials
+    toks = np.array([[st.sot, st.lang_token("en"), st.transcribe] + list(range(700, 760))] * 2)
+    a, b = _both(eng, enc, W, 8, lambda: eng.forward([1, 3], toks)[0].cpu().numpy())
+    encf = enc.float().cpu().numpy()
+    scale = max(np.abs(a).max(), 1.0)
+    assert np.abs(a - b).max() < 0.02 * scale, np.abs(a - b).max()
+    for i, w in enumerate((1, 3)):
+        ref, _ = orc.decode(toks[i:i + 1], orc.cross_kv(encf[w:w + 1]))
+        assert np.abs(b[i] - ref[0]).max() < 0.02 * np.abs(ref).max() + 1e-3
+
+
+def test_factored_alignment_capture(small_models):
+    """Alignment-head probabilities: raw scores from the attention kernel, normalised by the split merge."""
+    dims, eng, enc, orc, W = small_models
+    st = dims.specials
+    toks = np.array([[st.sot, st.lang_token("en"), st.transcribe, st.no_timestamps] + list(range(1000, 1030)) + [st.eot]])
+    heads = dims.default_alignment_heads()
+    a, b = _both(eng, enc, W, 8, lambda: eng.forward([2], toks, align_heads=heads)[1][0].cpu().numpy())
+    assert np.allclose(b.sum(-1), 1.0, atol=1e-4)
+    assert np.abs(a - b).max() < 2e-3
+    _, _, cw = orc.decode(toks, orc.cross_kv(enc.float().cpu().numpy()[2:3]), return_cross_attn=True)
+    ref = np.stack([cw[l][0, h] for l, h in heads], 1)
+    assert np.abs(b - ref).max() < 2e-3
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0)], ids=["greedy", "beam5"])
+def test_factored_generate_matches_projected(small_models, kw):
+    dims, eng, enc, orc, W = small_models
+    st = dims.specials
+    prompt = [st.sot, st.lang_token("en"), st.transcribe]
+
+    def run():
+        return eng.generate(list(range(W)), [prompt] * W, suppress_tokens=_sup(st), max_length=100, **kw)
+
+    (ra, sa), (rb, sb) = _both(eng, enc, W, 5 * W, run)
+    same = sum(x.tokens == y.tokens for x, y in zip(ra, rb))
+    assert same >= W - 1, f"{same}/{W} windows identical"
+    for x, y in zip(ra, rb):
+        assert abs(x.no_speech_prob - y.no_speech_prob) < 2e-3
+        if x.tokens == y.tokens:
+            assert abs(x.score - y.score) < 2e-2 * max(1.0, abs(x.score))
+    assert sum(len(r.tokens) for r in rb) > W * 5
+
+
+def test_factored_prompted_prefill(small_models):
+    """A long previous-text prompt: many rows per window (m-tiles > 1, fewer key splits)."""
+    dims, eng, enc, orc, W = small_models
+    st = dims.specials
+    prompt = [st.sot_prev] + list(range(400, 500)) + [st.sot, st.lang_token("en"), st.transcribe]
+    a, b = _both(eng, enc, W, 5 * W, lambda: eng.generate([0, 2], [prompt] * 2, beam_size=5, patience=1.0,
+                                                            suppress_tokens=_sup(st), max_length=180)[0])
+    assert sum(x.tokens == y.tokens for x, y in zip(a, b)) >= 1
+    for x, y in zip(a, b):
+        assert abs(x.no_speech_prob - y.no_speech_prob) < 2e-3
+
+
+def test_large_v3_factored_matches_projected():
+    """The bench instantiation (d = 1280: 8 waves x 160 columns), projected vs factored on the GPU."""
+    W = 3
+    dims, sd, eng, enc = _engine("large-v3", 1, W, eot_after=30)
+    del sd
+    st = dims.specials
+    toks = np.array([[st.sot, st.lang_token("en"), st.transcribe] + list(range(300, 330))])
+    a, b = _both(eng, enc, W, 5 * W, lambda: eng.forward([2], toks)[0].cpu().numpy())
+    assert np.abs(a - b).max() < 0.02 * max(np.abs(a).max(), 1.0), np.abs(a - b).max()
+    prompt = [st.sot, st.lang_token("en"), st.transcribe]
+
+    def run():
+        return eng.generate(list(range(W)), [prompt] * W, suppress_tokens=_sup(st), max_length=80)[0]
+
+    ra, rb = _both(eng, enc, W, 5 * W, run)
+    assert sum(x.tokens == y.tokens for x, y in zip(ra, rb)) >= W - 1
+    assert sum(len(r.tokens) for r in rb) > W * 5
+    eng.set_option("cross_mode", 1)
+    assert eng.device_bytes() > 0

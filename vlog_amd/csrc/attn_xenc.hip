@@ -1,0 +1,574 @@
+// Factored cross-attention for the decoder (gfx950): attend over the encoder output itself, not over a
+// projected cross-KV cache.
+//
+// For head h, Whisper's cross-attention reads K_h = E Wk_h^T and V_h = E Wv_h^T + bv_h, where E is the
+// window's encoder output [1500][d] and Wk_h, Wv_h are rows h*64 .. h*64+63 of the k/v projections
+// (modeling_whisper.py:241-356 [TF]; CTranslate2 projects them once per window [FW↑]).  Reassociated:
+//   s_h[t] = q_h . K_h[t]          = (Wk_h^T q_h) . E[t]             q'_h = Wk_h^T q_h   (a d-vector)
+//   o_h    = sum_t p_h[t] V_h[t]   = Wv_h (sum_t p_h[t] E[t]) + bv_h  u_h  = P_h E         (a d-vector)
+// (the softmax row sums to 1, so the v bias passes through unchanged).  Per decoder step and layer, a
+// window's attention then streams E ONCE for every head and every row of the window: 1500 x d bf16 =
+// 3.84 MB for large-v3, against 2 x 3.84 MB of K and V panels.  The per-window cross-KV projection
+// disappears too (314.6 GFLOP and 245.8 MB of HBM per large-v3 window).  The price is H x the attention
+// FLOPs: a (H R) x 1500 x d GEMM pair per window and layer (R = rows sharing the window), which MFMA
+// absorbs.  At R = 1 the kernel executes 64 FLOP per streamed byte (20 of its 32 MFMA rows used), far
+// under the ~312 FLOP/B ridge of MI355X, so it stays HBM-bound.
+//
+// Three kernels per layer:
+//   xq_kernel       q' = (1/8 log2 e) Wk_h^T q_h, bf16 [rows][H][d] (MFMA, K = 64).  Optionally sums the cq
+//                   projection's split-K slabs while loading q, in the order splitk_reduce_kernel uses.
+//   xattn_kernel    one workgroup per (window group, key split, m-tile of 32 (row, head) pairs).  NW waves
+//                   (8, or 4 when d/8 is not a multiple of 32), wave w owns the QW = d/NW columns
+//                   [w QW, (w+1) QW) of E.  Per 32-position tile:
+//                     S^T partial = E[t][wave cols] . q'^T  (v_mfma_f32_32x32x16_bf16, E from LDS as the A
+//                                   operand, q' register-resident as the B operand);
+//                     the NW partials are summed through LDS in a fixed order (two barriers per tile), so
+//                     every wave holds the same S^T and runs the same online softmax (deferred rescale,
+//                     log2 units);
+//                     U^T[wave cols] += E^T . P^T  (the S^T accumulator IS the P^T operand; E^T fragments
+//                                   come from the same LDS image through ds_read_b64_tr_b16).
+//                   E is streamed with coalesced 16-B non-temporal loads, register-staged one tile ahead,
+//                   into a wave-private LDS image, so no barrier guards it.  Output per split: (m, l) and
+//                   u / l as bf16.
+//   xcomb_vo_kernel merges the key splits (weights l_s 2^(m_s - M) / L) and applies Wv_h and bv_h (MFMA,
+//                   K = d) -> the attention output ao [rows][d].  With capture on, it also turns the raw
+//                   scores that xattn wrote for the alignment heads into probabilities.
+#include "common.h"
+#include <hip/hip_ext.h>
+#include <algorithm>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#define XTHR 8.0f              // deferred-rescale threshold (log2 units)
+#define XMAXS 16               // max key splits
+
+typedef __attribute__((ext_vector_type(4))) short xi16x4;
+typedef __attribute__((ext_vector_type(2))) int xi32x2;
+
+__device__ __forceinline__ f32x16 xzero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// E image in LDS: rows of LDR elements with LDR / 8 = 4 (mod 16) 16-B slots, and 16-B chunk c of row r
+// stored at chunk c ^ ((r >> 2) & 3) (a permutation inside each aligned quad of chunks).  Row r then starts
+// on slot 4r (mod 16) of the 256-B bank row, and both reads are conflict-free: ds_read_b128 of one chunk
+// over the 16 rows of a lane group (rows of equal r mod 4 differ in (r >> 2) & 3 inside every group of the
+// b128 lane-group table), and ds_read_b64_tr_b16 of 4 rows (4k..4k+3) x 64 B (slots 4i + quad).
+__device__ __forceinline__ int xchunk(int r, int c) { return c ^ ((r >> 2) & 3); }
+__host__ __device__ constexpr int xldr(int qw) { return (qw / 8 + ((4 - qw / 8) % 16 + 16) % 16) * 8; }
+
+// ------------------------------------------------------------------------------------------------------
+// Wk^T packing: wkt[l][h][c][j] = Wk_l[h*64 + j][c], from the fused [L][K|V][d][d] cross projection
+// (engine weight "dec.ckv.w").  Runs once per weight upload.
+__global__ void xpack_wkt_kernel(const bf16* __restrict__ ckv_w, bf16* __restrict__ wkt, int L, int H, int d) {
+  const long long total = (long long)L * H * d * 64;
+  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+    const int j = (int)(idx & 63);
+    const long long rest = idx >> 6;
+    const int c = (int)(rest % d);
+    const long long lh = rest / d;
+    const int h = (int)(lh % H), l = (int)(lh / H);
+    wkt[idx] = ckv_w[((long long)l * 2 * d + h * 64 + j) * d + c];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+struct XQArgs {
+  const bf16* q; long long ldq;          // q rows [rows][ldq] (unused when q_part is set)
+  const float* q_part; int q_splits, q_rows; const float* q_bias;   // cq split-K slabs [s][q_rows][ldq] + bias
+  const bf16* wkt;                       // this layer's Wk^T [H][d][64]
+  bf16* qp;                              // [rows][H][d]
+  int rows, H, d;
+  float scale;
+};
+
+// grid (ceil(rows / 32), H, ceil(d / 256)); wave w computes c-tiles 8z + 2w and 8z + 2w + 1 of head y for
+// 32 rows.  D[c][r] = sum_j Wk^T[c][j] q[r][h*64 + j]: A = Wk^T rows (16-B loads), B = q rows.  The block
+// first builds its 32 x 64 q tile in LDS: 8 elements per thread, every slab load issued before any add
+// (the slab sum is then one memory round trip, not one per slab), summed in slab order plus the bias as
+// splitk_reduce_kernel does, so the value is bit-identical to the unfused projection's bf16 q.
+__global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sq[32 * 72];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int h = blockIdx.y;
+  {
+    const int rr = tid >> 3, c8 = (tid & 7) * 8, r = blockIdx.x * 32 + rr;
+    bf16x8 qv = bf16x8{};
+    if (r < a.rows) {
+      const int col = h * 64 + c8;
+      if (a.q_part) {
+        const long long slab = (long long)a.q_rows * a.ldq;
+        const float* pq = a.q_part + (long long)r * a.ldq + col;
+        f32x4 lo[XMAXS], hi[XMAXS];
+#pragma unroll
+        for (int sp = 0; sp < XMAXS; ++sp)
+          if (sp < a.q_splits) {
+            lo[sp] = *(const f32x4*)(pq + sp * slab);
+            hi[sp] = *(const f32x4*)(pq + sp * slab + 4);
+          }
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sp = 0; sp < XMAXS; ++sp)
+          if (sp < a.q_splits) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { v[i] += lo[sp][i]; v[4 + i] += hi[sp][i]; }
+          }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qv[i] = f2bf(v[i] + a.q_bias[col + i]);
+      } else {
+        qv = *(const bf16x8*)(a.q + (long long)r * a.ldq + col);
+      }
+    }
+    *(bf16x8*)(sq + rr * 72 + c8) = qv;
+  }
+  __syncthreads();
+  const int r = blockIdx.x * 32 + l32;
+  bf16x8 qb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qb[s] = *(const bf16x8*)(sq + l32 * 72 + 16 * s + 8 * hh);
+  const int n_ct = a.d / 32;
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci) {
+    const int ct = blockIdx.z * 8 + wv * 2 + ci;
+    if (ct >= n_ct) break;
+    f32x16 acc = xzero16();
+    const bf16* wr = a.wkt + ((long long)h * a.d + ct * 32 + l32) * 64 + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(wr + 16 * s), qb[s], acc, 0, 0, 0);
+    if (r < a.rows) {
+      bf16* op = a.qp + ((long long)r * a.H + h) * a.d + ct * 32 + 4 * hh;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(acc[4 * g + e] * a.scale);
+        *(bf16x4*)(op + 8 * g) = w;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+struct XAttnArgs {
+  const bf16* qp;                        // [rows][H][d], pre-scaled (log2 units)
+  const bf16* enc;                       // [slots][T][d]
+  const int* hyp_slot; const int* row_hyp; const int* done;
+  int H, T, d, G, n_mt, splits, n_items, per_xcd;
+  long long slab_rows;                   // rows of the whole pass: partial slab stride
+  bf16* part_u;                          // [splits][slab_rows][H][d]   u_s / l_s
+  float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
+  float* probs; const int* head_map; int n_align;   // capture: raw scores [row][n_align][T]
+  unsigned long long* stat;
+};
+
+template <int QW, int NW>
+__global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
+  constexpr int KS = QW / 16, CT = QW / 32, LDR = xldr(QW), CPR = QW / 8;
+  __shared__ __attribute__((aligned(16))) char smem[NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  // XCD-aware item order: the blocks of one (group, split), i.e. its m-tiles, run on one XCD at about the
+  // same time, so the 2nd..n-th reads of an E tile hit that XCD's L2
+  const int item = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
+  if (item >= a.n_items) return;
+  const int mt = item % a.n_mt;
+  const int rest = item / a.n_mt;
+  const int split = rest % a.splits, grp = rest / a.splits;
+  const int M = a.G * a.H;
+  const int m = mt * 32 + l32;
+  const int row0 = grp * a.G;
+  int row = row0, hd = 0;
+  bool valid = m < M;
+  if (valid) {
+    const int ri = m / a.H;
+    row = row0 + ri;
+    hd = m - ri * a.H;
+    valid = !(a.done && a.done[a.row_hyp[row]]);
+  }
+  if (!__any(valid)) return;             // identical in all waves: uniform exit before any barrier
+  const int slot = a.hyp_slot[a.row_hyp[row0]];
+  const int n_tiles = (a.T + 31) / 32;
+  const int tb = split * n_tiles / a.splits, te = (split + 1) * n_tiles / a.splits;
+  const int cb = wv * QW;
+  const bf16* E = a.enc + (long long)slot * a.T * a.d + cb;
+  bf16* sE = (bf16*)smem + wv * 32 * LDR;
+  float* sX = (float*)(smem + NW * 32 * LDR * 2);        // [NW][16][64] S^T partials
+  float* sRed = sX + NW * 16 * 64;                       // [16][64] their sums
+  {
+    const unsigned long long nq = __popcll(__ballot(valid && hh == 0));
+    if (a.stat && tid == 0) {
+      const long long npos = (long long)min(te * 32, a.T) - tb * 32;
+      unsigned long long by = nq * (unsigned long long)a.d * 2;
+      if (mt == 0) by += (unsigned long long)(npos * a.d * 2);
+      atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), by);
+    }
+  }
+
+  bf16x8 qf[KS];
+  {
+    const bf16* qr = a.qp + ((long long)row * a.H + hd) * a.d + cb + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = valid ? *(const bf16x8*)(qr + 16 * s) : bf16x8{};
+  }
+  f32x16 o[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) o[c] = xzero16();
+  float m_run = -INFINITY, l_run = 0.f;
+
+  // Address arithmetic is recomputed from an opaque copy of the lane id inside the loop (`lo`), so the
+  // compiler does not hoist ~40 loop-invariant addresses into registers the accumulators need.
+  i32x4 stg[KS];
+  auto load = [&](int tile, int lo) {
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
+      const int t = min(tile * 32 + r, a.T - 1);
+      stg[i] = __builtin_nontemporal_load((const i32x4*)(E + (long long)t * a.d + ch * 8));
+    }
+  };
+  float* pr_row = nullptr;
+  if (a.probs && wv == 0 && valid) {
+    const int hm = a.head_map[hd];
+    if (hm >= 0) pr_row = a.probs + ((long long)row * a.n_align + hm) * a.T;
+  }
+  if (tb < te) load(tb, lane);
+  for (int tile = tb; tile < te; ++tile) {
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    // wave-private LDS image of this tile (this wave's earlier reads of it are complete: LDS is in order)
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
+      *(i32x4*)(sE + r * LDR + 8 * xchunk(r, ch)) = stg[i];
+    }
+    if (tile + 1 < te) load(tile + 1, lo);
+    // ---- S^T partial over this wave's columns
+    f32x16 sc = xzero16();
+    {
+      // A fragment of k-step s: row l32, chunk 2s + hh -> stored at 4 (s >> 1) + ((2 (s & 1) + hh) ^ g)
+      const int l32o = lo & 31, g = (l32o >> 2) & 3;
+      const bf16* s0 = sE + l32o * LDR + 8 * (hh ^ g);
+      const bf16* s1 = sE + l32o * LDR + 8 * ((2 + hh) ^ g);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 ea = *(const bf16x8*)(((s & 1) ? s1 : s0) + 32 * (s >> 1));
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ea, qf[s], sc, 0, 0, 0);
+      }
+    }
+    // the NW partials -> the full S^T in every wave: partials to LDS; wave w sums registers
+    // [w RPW, (w+1) RPW) over the waves in a fixed order (0..NW-1); every wave reads the 16 sums back
+    constexpr int RPW = 16 / NW;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sX[(wv * 16 + r) * 64 + lane] = sc[r];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      const int r = wv * RPW + k;
+      float v = sX[r * 64 + lane];
+#pragma unroll
+      for (int w2 = 1; w2 < NW; ++w2) v += sX[(w2 * 16 + r) * 64 + lane];
+      sRed[r * 64 + lane] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[r] = sRed[r * 64 + lane];
+    const int t0 = tile * 32;
+    if (t0 + 32 > a.T) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (t0 + 8 * (r >> 2) + 4 * hh + (r & 3) >= a.T) sc[r] = -INFINITY;
+    }
+    if (pr_row) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = t0 + 8 * (r >> 2) + 4 * hh + (r & 3);
+        if (t < a.T) pr_row[t] = sc[r];
+      }
+    }
+    // ---- online softmax (lane = one (row, head) column), deferred rescale
+    float mx = sc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (__any(mx > m_run + XTHR)) {
+      const float mn = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+      l_run *= alpha;
+#pragma unroll
+      for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+      m_run = mn;
+    }
+    bf16x8 pf[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(sc[r] - m_run);
+      l_run += p;
+      pf[r >> 3][r & 7] = f2bf(p);
+    }
+    // ---- U^T (wave cols) += E^T . P^T.  Transposed read of rows 16 ks + 8 jh + 4 hh + gq, columns
+    // 32 c + 16 (G4 & 1) + 4 gp: chunk 4 c + lowc (lowc = 2 (G4 & 1) + (gp >> 1)) is stored at
+    // 4 c + (lowc ^ (2 jh + hh)), so each jh has one base address and (ks, c) are immediate offsets.
+    {
+      const int G4 = (lo >> 4) & 3, gi = lo & 15, gq = gi >> 2, gp = gi & 3;
+      const int lowc = 2 * (G4 & 1) + (gp >> 1);
+      const bf16* tb0 = sE + (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
+      const bf16* tb1 = sE + (8 + 4 * hh + gq) * LDR + 8 * (lowc ^ (2 + hh)) + 4 * (gp & 1);
+#pragma unroll
+      for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int off = 16 * ks * LDR + 32 * c;
+          const xi32x2 v0 = __builtin_bit_cast(xi32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                            (__attribute__((address_space(3))) xi16x4*)(tb0 + off)));
+          const xi32x2 v1 = __builtin_bit_cast(xi32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                            (__attribute__((address_space(3))) xi16x4*)(tb1 + off)));
+          const bf16x8 va = __builtin_bit_cast(bf16x8, i32x4{v0[0], v0[1], v1[0], v1[1]});
+          o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[ks], o[c], 0, 0, 0);
+        }
+    }
+  }
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (valid) {
+    const float inv = 1.0f / l_run;
+    const long long pi = ((long long)split * a.slab_rows + row) * a.H + hd;
+    if (wv == 0 && hh == 0) {
+      a.part_ml[2 * pi] = m_run;
+      a.part_ml[2 * pi + 1] = l_run;
+    }
+    bf16* up = a.part_u + pi * a.d + cb + 4 * hh;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[c][4 * g + e] * inv);
+        *(bf16x4*)(up + 32 * c + 8 * g) = w;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+struct XCombArgs {
+  const bf16* part_u; const float* part_ml; int splits; long long slab_rows;
+  const bf16* wv; const float* bv;       // this layer's V projection [d][d] (row h*64 + j) and bias [d]
+  const int* row_hyp; const int* done;
+  bf16* out; long long ldo;
+  int rows, H, d, T;
+  float* probs; const int* head_map; int n_align;
+};
+
+// grid (ceil(rows / 32), H), 8 waves.  D[r][j] = sum_c u[r][h][c] Wv[h*64 + j][c]: A = merged u rows (built
+// from the bf16 split partials while loading), B = Wv rows.  Wave w reduces c in [w d/8, (w+1) d/8): its
+// partial and weight loads are issued KB k-steps at a time (one memory round trip per batch, not per
+// k-step).  The merged u is split into bf16 hi + lo parts (two MFMAs), so the V projection sees u to
+// ~16 bits instead of 8.  The 8 partial products are summed through LDS in a fixed order.
+template <int KS8, int MAXS>
+__global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
+  constexpr int KB = (16 / MAXS) < KS8 ? (16 / MAXS) : KS8;   // k-steps per load batch (<= 16 partial loads)
+  __shared__ float sR[8][2][16][64];
+  __shared__ float sML[32][2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int h = blockIdx.y;
+  const int r = blockIdx.x * 32 + l32;
+  const bool valid = r < a.rows && !(a.done && a.done[a.row_hyp[r]]);
+  const long long sstride = a.slab_rows * a.H;          // (row, head) pairs per split slab
+  float w[MAXS];
+  float Mx = -INFINITY, L = 0.f;
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) w[s] = 0.f;
+  if (valid) {
+    const float* ml = a.part_ml + 2 * ((long long)r * a.H + h);
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+      if (s < a.splits) Mx = fmaxf(Mx, ml[2 * s * sstride]);
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+      if (s < a.splits) {
+        w[s] = ml[2 * s * sstride + 1] * __builtin_amdgcn_exp2f(ml[2 * s * sstride] - Mx);
+        L += w[s];
+      }
+    const float inv = 1.0f / L;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) w[s] *= inv;
+  }
+  f32x16 acc[2] = {xzero16(), xzero16()};
+  const int cb = wv * (KS8 * 16);
+  const bf16* pu = a.part_u + ((long long)min(r, a.rows - 1) * a.H + h) * a.d + cb + 8 * hh;
+  const bf16* w0 = a.wv + (long long)(h * 64 + l32) * a.d + cb + 8 * hh;
+  const bf16* w1 = w0 + 32LL * a.d;
+  const long long pstride = sstride * a.d;
+#pragma unroll
+  for (int s0 = 0; s0 < KS8; s0 += KB) {
+    bf16x8 pv[KB][MAXS], wa[KB], wb[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      if (s0 + k >= KS8) break;
+      wa[k] = *(const bf16x8*)(w0 + 16 * (s0 + k));
+      wb[k] = *(const bf16x8*)(w1 + 16 * (s0 + k));
+#pragma unroll
+      for (int sp = 0; sp < MAXS; ++sp)
+        if (sp < a.splits) pv[k][sp] = *(const bf16x8*)(pu + sp * pstride + 16 * (s0 + k));
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      if (s0 + k >= KS8) break;
+      float u[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sp = 0; sp < MAXS; ++sp)
+        if (sp < a.splits) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) u[i] = fmaf(w[sp], bf2f(pv[k][sp][i]), u[i]);
+        }
+      bf16x8 uh, ul;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uh[i] = f2bf(u[i]);
+        ul[i] = f2bf(u[i] - bf2f(uh[i]));
+      }
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, wa[k], acc[0], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul, wa[k], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, wb[k], acc[1], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul, wb[k], acc[1], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sR[wv][jt][i][lane] = acc[jt][i];
+  if (wv == 0 && hh == 0) {
+    sML[l32][0] = Mx;
+    sML[l32][1] = L;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < 2 * 16 * 64; idx += 512) {
+    const int jt = idx >> 10, i = (idx >> 6) & 15, ln = idx & 63;
+    float v = sR[0][jt][i][ln];
+#pragma unroll
+    for (int w2 = 1; w2 < 8; ++w2) v += sR[w2][jt][i][ln];
+    const int j = 32 * jt + (ln & 31);
+    const int rr = blockIdx.x * 32 + 8 * (i >> 2) + 4 * (ln >> 5) + (i & 3);
+    if (rr < a.rows && !(a.done && a.done[a.row_hyp[rr]]))
+      a.out[(long long)rr * a.ldo + h * 64 + j] = f2bf(v + a.bv[h * 64 + j]);
+  }
+  if (a.probs) {
+    const int hm = a.head_map[h];
+    if (hm >= 0) {
+      for (int idx = tid; idx < 32 * a.T; idx += 512) {
+        const int ri = idx / a.T, t = idx - ri * a.T;
+        const int rr = blockIdx.x * 32 + ri;
+        if (rr >= a.rows) continue;
+        float* p = a.probs + ((long long)rr * a.n_align + hm) * a.T + t;
+        *p = __builtin_amdgcn_exp2f(*p - sML[ri][0]) / sML[ri][1];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// host launchers
+
+void launch_xpack_wkt(const bf16* ckv_w, bf16* wkt, int L, int H, int d, hipStream_t st) {
+  const long long total = (long long)L * H * d * 64;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(xpack_wkt_kernel, dim3(blocks), dim3(256), 0, st, ckv_w, wkt, L, H, d);
+  WM_LAUNCH_CHECK("xpack_wkt_kernel");
+}
+
+void launch_xq(const bf16* q, long long ldq, const CrossFuse& fz, const bf16* wkt, bf16* qp, int rows, int H, int d,
+               hipStream_t st) {
+  if (rows <= 0) return;
+  if (d != H * 64) throw std::runtime_error("xq: n_state must be n_head * 64");
+  if (fz.q_part && fz.q_splits > XMAXS) throw std::runtime_error("xq: too many cq split-K slabs");
+  XQArgs a{};
+  a.q = q; a.ldq = ldq; a.q_part = fz.q_part; a.q_splits = fz.q_splits; a.q_rows = fz.q_rows; a.q_bias = fz.q_bias;
+  a.wkt = wkt; a.qp = qp; a.rows = rows; a.H = H; a.d = d;
+  a.scale = 0.125f * 1.4426950408889634f;
+  const dim3 grid((rows + 31) / 32, H, (d / 32 + 7) / 8);
+  hipLaunchKernelGGL(xq_kernel, grid, dim3(256), 0, st, a);
+  WM_LAUNCH_CHECK("xq_kernel");
+}
+
+// Key splits of a pass.  A function of the whole pass, so slicing a pass into launches never changes a
+// row's arithmetic: about three rounds of 256 one-workgroup CUs, at most 16, at least one 32-position tile
+// per split, and the bf16 partial slabs capped at 256 MB.
+int xattn_splits(int plan_rows, int group, int H, int T, int d) {
+  static const int forced = [] {
+    const char* e = std::getenv("VLOG_AMD_XSPLITS");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int groups = std::max(1, plan_rows / std::max(group, 1));
+  const long long n_mt = ((long long)group * H + 31) / 32;
+  const long long items = groups * n_mt;
+  const int n_tiles = (T + 31) / 32;
+  int s = (int)((768 + items / 2) / items);
+  if (forced > 0) s = forced;
+  s = std::max(1, std::min(s, std::min(XMAXS, n_tiles)));
+  const long long slab = (long long)plan_rows * H * d * 2;
+  while (s > 1 && slab * s > (256LL << 20)) --s;
+  return s;
+}
+
+void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const int* row_hyp, const int* done, int rows,
+                  long long slab_rows, int group, int H, int T, int d, int splits, bf16* part_u, float* part_ml,
+                  float* probs, const int* head_map, int n_align, unsigned long long* stat, hipStream_t st,
+                  hipEvent_t ev0, hipEvent_t ev1) {
+  if (rows <= 0) return;
+  if (group <= 0 || rows % group != 0) throw std::runtime_error("xattn: rows must be a multiple of the group");
+  if (splits < 1 || splits > XMAXS || splits > (T + 31) / 32) throw std::runtime_error("xattn: bad key splits");
+  XAttnArgs a{};
+  a.qp = qp; a.enc = enc; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
+  a.H = H; a.T = T; a.d = d; a.G = group; a.n_mt = (group * H + 31) / 32; a.splits = splits;
+  const long long items = (long long)(rows / group) * a.n_mt * splits;
+  if (items > (1LL << 30)) throw std::runtime_error("xattn: too many work items");
+  a.n_items = (int)items;
+  a.per_xcd = (a.n_items + 7) / 8;
+  a.slab_rows = slab_rows; a.part_u = part_u; a.part_ml = part_ml;
+  a.probs = probs; a.head_map = head_map; a.n_align = n_align; a.stat = stat;
+  const dim3 grid(a.per_xcd * 8);
+#define XA_LAUNCH(QW_, NW_)                                                                                \
+  if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a);   \
+  else hipLaunchKernelGGL((xattn_kernel<QW_, NW_>), grid, dim3(NW_ * 64), 0, st, a);
+  switch (d) {                           // 8 waves of d/8 columns (registers: no spills), 4 for tiny
+    case 384: XA_LAUNCH(96, 4); break;
+    case 512: XA_LAUNCH(64, 8); break;
+    case 768: XA_LAUNCH(96, 8); break;
+    case 1024: XA_LAUNCH(128, 8); break;
+    case 1280: XA_LAUNCH(160, 8); break;
+    default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
+  }
+#undef XA_LAUNCH
+  WM_LAUNCH_CHECK("xattn_kernel");
+}
+
+void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long long slab_rows, const bf16* wv,
+                     const float* bv, const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H,
+                     int d, int T, float* probs, const int* head_map, int n_align, hipStream_t st) {
+  if (rows <= 0) return;
+  XCombArgs a{};
+  a.part_u = part_u; a.part_ml = part_ml; a.splits = splits; a.slab_rows = slab_rows; a.wv = wv; a.bv = bv;
+  a.row_hyp = row_hyp; a.done = done; a.out = out; a.ldo = ldo; a.rows = rows; a.H = H; a.d = d; a.T = T;
+  a.probs = probs; a.head_map = head_map; a.n_align = n_align;
+  const dim3 grid((rows + 31) / 32, H);
+#define XC_LAUNCH(KS8_)                                                                                  \
+  if (splits <= 1) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 1>), grid, dim3(512), 0, st, a);             \
+  else if (splits <= 2) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 2>), grid, dim3(512), 0, st, a);        \
+  else if (splits <= 4) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 4>), grid, dim3(512), 0, st, a);        \
+  else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, XMAXS>), grid, dim3(512), 0, st, a);
+  switch (d) {                           // 8 waves x d/8 columns of the reduction: d/128 k-steps each
+    case 384: XC_LAUNCH(3); break;
+    case 512: XC_LAUNCH(4); break;
+    case 768: XC_LAUNCH(6); break;
+    case 1024: XC_LAUNCH(8); break;
+    case 1280: XC_LAUNCH(10); break;
+    default: throw std::runtime_error("xcomb_vo: unsupported n_state " + std::to_string(d));
+  }
+#undef XC_LAUNCH
+  WM_LAUNCH_CHECK("xcomb_vo_kernel");
+}

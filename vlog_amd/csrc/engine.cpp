@@ -40,6 +40,15 @@ void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, co
                        long long, int, int, int, float*, float*, float*, float*, const int*, int, int, int,
                        const CrossFuse&, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 
+// factored cross-attention over the encoder output (attn_xenc.hip)
+void launch_xpack_wkt(const bf16*, bf16*, int, int, int, hipStream_t);
+void launch_xq(const bf16*, long long, const CrossFuse&, const bf16*, bf16*, int, int, int, hipStream_t);
+int xattn_splits(int, int, int, int, int);
+void launch_xattn(const bf16*, const bf16*, const int*, const int*, const int*, int, long long, int, int, int, int, int,
+                  bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
+void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, const float*, const int*, const int*, bf16*,
+                     long long, int, int, int, int, float*, const int*, int, hipStream_t);
+
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
 void launch_dtw(const float*, int, int, float*, signed char*, int*, int*, int*, hipStream_t);
@@ -47,10 +56,10 @@ void launch_dtw(const float*, int, int, float*, signed char*, int*, int*, int*, 
 // Kernel classes timed by the built-in profiler (wm_profile / wm_profile_read).
 enum ProfClass {
   P_LOGMEL = 0, P_ENC_GEMM, P_ENC_ATTN, P_ENC_OTHER, P_CROSSKV_GEMM, P_DEC_GEMM, P_SELF_ATTN, P_CROSS_ATTN,
-  P_LOGITS_GEMM, P_SELECT, P_DEC_OTHER, P_N
+  P_LOGITS_GEMM, P_SELECT, P_DEC_OTHER, P_CROSS_COMB, P_N
 };
 static const char* kProfNames[P_N] = {"logmel", "enc_gemm", "enc_attn", "enc_other", "crosskv_gemm", "dec_gemm",
-                                      "self_attn", "cross_attn", "logits_gemm", "select", "dec_other"};
+                                      "self_attn", "cross_attn", "logits_gemm", "select", "dec_other", "cross_comb"};
 
 namespace {
 
@@ -132,6 +141,14 @@ struct wm_engine {
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
   DevBuf d_cross_cnt;        // its per-(row, head) arrival counters (zeroed at allocation, reset in-kernel)
+  // cross-attention form: 1 = factored (attention over the encoder output, attn_xenc.hip: a window's slot
+  // holds its encoder output, 3.84 MB for large-v3), 0 = projected cross-KV panels (attn_dec.hip: 245.8 MB
+  // per large-v3 window, projected by wm_cross_kv)
+  int cross_mode = 1;
+  DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs
+  DevBuf xwkt;               // factored: Wk^T per layer and head [L][H][d][64] bf16, packed from dec.ckv.w
+  bool xwkt_ready = false;
+  DevBuf s_qp, s_pu, s_pml;  // factored step scratch: q' [rows][H][d], split partials u/l and (m, l)
   int cross_cap = 0;         // cross-attention grid cap (0: one block per item; >0: persistent grid-stride form,
                              // 2 blocks/CU measured ~2 % faster alone but slower with the fused q combine)
   hipStream_t st2 = nullptr;
@@ -162,7 +179,7 @@ struct wm_engine {
 
   size_t device_bytes() const {
     size_t t = arena.bytes;
-    for (const DevBuf* b : {&e_cols, &e_h1, &e_x, &e_hb, &e_qkv, &e_ao, &e_ff, &ckv, &skv, &s_x, &s_hb, &s_q, &s_ao,
+    for (const DevBuf* b : {&e_cols, &e_h1, &e_x, &e_hb, &e_qkv, &e_ao, &e_ff, &ckv, &xenc, &xwkt, &s_qp, &s_pu, &skv, &s_x, &s_hb, &s_q, &s_ao,
                             &s_ff, &s_logits, &s_pm, &s_pl, &s_po, &d_tokens, &d_lin, &d_fin_tok})
       t += b->bytes;
     return t;
@@ -496,7 +513,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     }
     gemm(amat(hb, d), W.cq_w, d, d, d, ep);
   }
-  if (e->cross_fuse & 2) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
+  if ((e->cross_fuse & 2) && e->cross_mode == 0) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   float* probs = nullptr;
   const int* hmap = nullptr;
   if (attn && align_map) {
@@ -510,7 +527,31 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     }
   }
   if (mid) HIP_OK(hipEventRecord(mid, st));
-  {
+  if (e->cross_mode == 1) {
+    // factored: q' = Wk_h^T q_h, attention over the encoder output, split merge + Wv_h (attn_xenc.hip)
+    const int splits = xattn_splits(sl.total_rows, cross_group, H, T, d);
+    const size_t prow = (size_t)H * d;
+    bf16* qp = e->s_qp.as<bf16>() + (size_t)r0 * prow;
+    bf16* pu = e->s_pu.as<bf16>() + (size_t)r0 * prow;
+    float* pml = e->s_pml.as<float>() + (size_t)r0 * H * 2;
+    const bf16* wkt = e->xwkt.as<bf16>() + (size_t)l * H * d * 64;
+    const bf16* wv = e->Wb("dec.ckv.w") + ((size_t)l * 2 * d + d) * d;
+    const float* bv = e->Wf("dec.ckv.b") + (size_t)l * 2 * d + d;
+    {
+      ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * H * d * 64, 2.0 * H * d * 64 + 2.0 * rows * d + 2.0 * rows * prow);
+      launch_xq(q, d, fz, wkt, qp, rows, H, d, st);
+    }
+    {
+      ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
+      launch_xattn(qp, e->xenc.as<bf16>(), e->d_hyp_slot.as<int>(), row_hyp, done, rows, sl.total_rows, cross_group, H, T,
+                   d, splits, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+    }
+    {
+      ProfScope ps(e, P_CROSS_COMB, st, 2.0 * rows * d * d, 2.0 * d * d + 2.0 * splits * rows * prow + 2.0 * rows * d);
+      launch_xcomb_vo(pu, pml, splits, sl.total_rows, wv, bv, row_hyp, done, ao, d, rows, H, d, T, probs, hmap, n_align,
+                      st);
+    }
+  } else {
     const size_t po = (size_t)r0 * H * 16;
     ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
     launch_cross_attn(q, d, ckv + (size_t)(2 * l) * ckv_layer, ckv + (size_t)(2 * l + 1) * ckv_layer, T,
@@ -551,6 +592,22 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
   const auto& m = e->dm;
   const int d = m.n_state, L = m.n_dec_layer;
   const auto& W0 = dec_weights(e)[0];
+  if (e->cross_mode == 1) {
+    // factored cross-attention scratch for the whole pass (slices index it by absolute row), and the
+    // per-head Wk^T layout (packed once per upload of dec.ckv.w)
+    const int H = m.n_head, T = m.n_audio_ctx;
+    const size_t prow = (size_t)H * d;
+    const int splits = xattn_splits(rows, cross_group, H, T, d);
+    e->s_qp.ensure((size_t)rows * prow * 2);
+    e->s_pu.ensure((size_t)splits * rows * prow * 2);
+    e->s_pml.ensure((size_t)splits * rows * H * 2 * 4);
+    if (!e->xwkt_ready) {
+      e->xwkt.ensure((size_t)L * H * d * 64 * 2);
+      launch_xpack_wkt(e->Wb("dec.ckv.w"), e->xwkt.as<bf16>(), L, H, d, st);
+      e->xwkt_ready = true;
+    }
+    if (!e->xenc.p) throw std::runtime_error("decoder: no encoder slots (wm_reserve + wm_cross_kv first)");
+  }
   int h0 = (rows / 2 / cross_group) * cross_group;
   const bool split = e->dec_split && logit_rows == nullptr && n_logit == rows && attn == nullptr && h0 >= 16 &&
                      rows - h0 >= 16;
@@ -613,10 +670,11 @@ void reserve(wm_engine* e, int n_slots, int n_hyp) {
   const auto& m = e->dm;
   const int H = m.n_head, C = m.n_text_ctx, T = m.n_audio_ctx, L = m.n_dec_layer;
   if (n_slots > e->n_slots) {
-    DevBuf nb;
-    nb.ensure((size_t)L * 2 * n_slots * H * T * 64 * 2);
+    // factored mode keeps each window's encoder output (T x d bf16); projected mode its L x 2 K/V panels
     e->ckv.release();
-    e->ckv = nb;
+    e->xenc.release();
+    if (e->cross_mode == 1) e->xenc.ensure((size_t)n_slots * T * m.n_state * 2);
+    else e->ckv.ensure((size_t)L * 2 * n_slots * H * T * 64 * 2);
     e->n_slots = n_slots;
   }
   if (n_hyp > e->n_hyp_cap) {
@@ -950,6 +1008,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("VLOG_AMD_CROSS_MODE")) e->cross_mode = std::atoi(v) != 0;
     try {
       build_layout(e);
       build_frontend(e, nullptr);
@@ -975,7 +1034,8 @@ void wm_destroy(wm_engine* e) {
                     &e->d_row_pos, &e->d_row_hyp, &e->d_hyp_slot, &e->d_n_active, &e->d_suppress, &e->d_cand_tok,
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
-                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt})
+                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt,
+                    &e->xenc, &e->xwkt, &e->s_qp, &e->s_pu, &e->s_pml})
     b->release();
   if (e->st2) (void)hipStreamDestroy(e->st2);
   for (hipEvent_t ev : {e->ev_fork, e->ev_mid, e->ev_join})
@@ -992,6 +1052,7 @@ int wm_set_weight(wm_engine* e, const char* name, const void* d_src, int64_t nby
                                " bytes, got " + std::to_string(nbytes));
     HIP_OK(hipMemcpyAsync((char*)e->arena.p + it->second.off, d_src, nbytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     it->second.set = true;
+    if (it->first == "dec.ckv.w") e->xwkt_ready = false;
   });
 }
 
@@ -1061,6 +1122,13 @@ int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void*
     if (slot0 < 0 || slot0 + B > e->n_slots) throw std::runtime_error("wm_cross_kv: slots out of range (wm_reserve first)");
     const auto& m = e->dm;
     const int d = m.n_state, T = m.n_audio_ctx;
+    if (e->cross_mode == 1) {   // factored: the slot holds the encoder output itself
+      const size_t per = (size_t)T * d;
+      ProfScope ps(e, P_CROSSKV_GEMM, (hipStream_t)stream, 0, 2.0 * 2 * B * per);
+      HIP_OK(hipMemcpyAsync(e->xenc.as<bf16>() + (size_t)slot0 * per, d_enc, (size_t)B * per * 2,
+                            hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      return;
+    }
     GemmEpi ep = epi_of(EPI_CROSS_KV, e->ckv.p, 0, e->Wf("dec.ckv.b"));
     ep.rpb = T; ep.d = d; ep.head_dim = 64; ep.n_head = m.n_head; ep.n_slots = e->n_slots; ep.slot0 = slot0;
     gemm_p(e, P_CROSSKV_GEMM, amat((const bf16*)d_enc, d), e->Wb("dec.ckv.w"), d, B * T, m.n_dec_layer * 2 * d, d, ep,
@@ -1120,6 +1188,19 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
+    else if (k == "cross_mode") {
+      // switching re-allocates the window slots in the new form (their contents are dropped: run
+      // wm_cross_kv again)
+      const int v = value ? 1 : 0;
+      if (v != e->cross_mode) {
+        HIP_OK(hipDeviceSynchronize());
+        e->cross_mode = v;
+        const int n = e->n_slots;
+        e->n_slots = 0;
+        if (n > 0) reserve(e, n, e->n_hyp_cap);
+        else { e->ckv.release(); e->xenc.release(); }
+      }
+    }
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }
