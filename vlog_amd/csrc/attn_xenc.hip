@@ -62,17 +62,32 @@ __device__ __forceinline__ int xchunk(int r, int c) { return c ^ ((r >> 2) & 3);
 __host__ __device__ constexpr int xldr(int qw) { return (qw / 8 + ((4 - qw / 8) % 16 + 16) % 16) * 8; }
 
 // ------------------------------------------------------------------------------------------------------
-// Wk^T packing: wkt[l][h][c][j] = Wk_l[h*64 + j][c], from the fused [L][K|V][d][d] cross projection
-// (engine weight "dec.ckv.w").  Runs once per weight upload.
-__global__ void xpack_wkt_kernel(const bf16* __restrict__ ckv_w, bf16* __restrict__ wkt, int L, int H, int d) {
+// Weight packing, from the fused [L][K|V][d][d] cross projection (engine weight "dec.ckv.w"); runs once per
+// weight upload:
+//   wkt[l][h][c][j]            = Wk_l[h*64 + j][c]   (xq's A operand: 64 contiguous j per c)
+//   wvb[l][h][c/16][j][c%16]   = Wv_l[h*64 + j][c]   (xcomb's B operand: one k-step of 32 j = 1 KB contiguous)
+__global__ void xpack_kernel(const bf16* __restrict__ ckv_w, bf16* __restrict__ wkt, bf16* __restrict__ wvb, int L,
+                             int H, int d) {
   const long long total = (long long)L * H * d * 64;
   for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-    const int j = (int)(idx & 63);
-    const long long rest = idx >> 6;
-    const int c = (int)(rest % d);
-    const long long lh = rest / d;
-    const int h = (int)(lh % H), l = (int)(lh / H);
-    wkt[idx] = ckv_w[((long long)l * 2 * d + h * 64 + j) * d + c];
+    {
+      const int j = (int)(idx & 63);
+      const long long rest = idx >> 6;
+      const int c = (int)(rest % d);
+      const long long lh = rest / d;
+      const int h = (int)(lh % H), l = (int)(lh / H);
+      wkt[idx] = ckv_w[((long long)l * 2 * d + h * 64 + j) * d + c];
+    }
+    {
+      const int c16 = (int)(idx & 15);
+      const long long r1 = idx >> 4;
+      const int j = (int)(r1 & 63);
+      const long long r2 = r1 >> 6;
+      const int kb = (int)(r2 % (d / 16));
+      const long long lh = r2 / (d / 16);
+      const int h = (int)(lh % H), l = (int)(lh / H);
+      wvb[idx] = ckv_w[((long long)l * 2 * d + d + h * 64 + j) * d + kb * 16 + c16];
+    }
   }
 }
 
@@ -95,33 +110,41 @@ __global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 sq[32 * 72];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
   const int h = blockIdx.y;
+  const int n_ct = a.d / 32;
+  // this wave's Wk^T fragments first (independent of q: one memory round trip with the q loads)
+  bf16x8 wf[2][4];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci) {
+    const int ct = min(blockIdx.z * 8 + wv * 2 + ci, n_ct - 1);
+    const bf16* wr = a.wkt + ((long long)h * a.d + ct * 32 + l32) * 64 + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) wf[ci][s] = *(const bf16x8*)(wr + 16 * s);
+  }
   {
-    const int rr = tid >> 3, c8 = (tid & 7) * 8, r = blockIdx.x * 32 + rr;
-    bf16x8 qv = bf16x8{};
-    if (r < a.rows) {
-      const int col = h * 64 + c8;
-      if (a.q_part) {
-        const long long slab = (long long)a.q_rows * a.ldq;
-        const float* pq = a.q_part + (long long)r * a.ldq + col;
-        f32x4 lo[XMAXS], hi[XMAXS];
+    const int rr = tid >> 3, c8 = (tid & 7) * 8, r = min(blockIdx.x * 32 + rr, a.rows - 1);
+    bf16x8 qv;
+    const int col = h * 64 + c8;
+    if (a.q_part) {
+      const long long slab = (long long)a.q_rows * a.ldq;
+      const float* pq = a.q_part + (long long)r * a.ldq + col;
+      f32x4 lo[XMAXS], hi[XMAXS];
 #pragma unroll
-        for (int sp = 0; sp < XMAXS; ++sp)
-          if (sp < a.q_splits) {
-            lo[sp] = *(const f32x4*)(pq + sp * slab);
-            hi[sp] = *(const f32x4*)(pq + sp * slab + 4);
-          }
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < XMAXS; ++sp)
+        if (sp < a.q_splits) {
+          lo[sp] = *(const f32x4*)(pq + sp * slab);
+          hi[sp] = *(const f32x4*)(pq + sp * slab + 4);
+        }
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int sp = 0; sp < XMAXS; ++sp)
-          if (sp < a.q_splits) {
+      for (int sp = 0; sp < XMAXS; ++sp)
+        if (sp < a.q_splits) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { v[i] += lo[sp][i]; v[4 + i] += hi[sp][i]; }
-          }
+          for (int i = 0; i < 4; ++i) { v[i] += lo[sp][i]; v[4 + i] += hi[sp][i]; }
+        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) qv[i] = f2bf(v[i] + a.q_bias[col + i]);
-      } else {
-        qv = *(const bf16x8*)(a.q + (long long)r * a.ldq + col);
-      }
+      for (int i = 0; i < 8; ++i) qv[i] = f2bf(v[i] + a.q_bias[col + i]);
+    } else {
+      qv = *(const bf16x8*)(a.q + (long long)r * a.ldq + col);
     }
     *(bf16x8*)(sq + rr * 72 + c8) = qv;
   }
@@ -130,16 +153,13 @@ __global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
   bf16x8 qb[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qb[s] = *(const bf16x8*)(sq + l32 * 72 + 16 * s + 8 * hh);
-  const int n_ct = a.d / 32;
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci) {
     const int ct = blockIdx.z * 8 + wv * 2 + ci;
     if (ct >= n_ct) break;
     f32x16 acc = xzero16();
-    const bf16* wr = a.wkt + ((long long)h * a.d + ct * 32 + l32) * 64 + 8 * hh;
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(wr + 16 * s), qb[s], acc, 0, 0, 0);
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ci][s], qb[s], acc, 0, 0, 0);
     if (r < a.rows) {
       bf16* op = a.qp + ((long long)r * a.H + h) * a.d + ct * 32 + 4 * hh;
 #pragma unroll
@@ -160,13 +180,13 @@ struct XAttnArgs {
   const int* hyp_slot; const int* row_hyp; const int* done;
   int H, T, d, G, n_mt, splits, n_items, per_xcd;
   long long slab_rows;                   // rows of the whole pass: partial slab stride
-  bf16* part_u;                          // [splits][slab_rows][H][d]   u_s / l_s
+  bf16* part_u;                          // [splits][H][d/16][slab_rows][16]   u_s / l_s
   float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
   float* probs; const int* head_map; int n_align;   // capture: raw scores [row][n_align][T]
   unsigned long long* stat;
 };
 
-template <int QW, int NW>
+template <int QW, int NW, int DEPTH>
 __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   constexpr int KS = QW / 16, CT = QW / 32, LDR = xldr(QW), CPR = QW / 8;
   __shared__ __attribute__((aligned(16))) char smem[NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4];
@@ -221,8 +241,8 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 
   // Address arithmetic is recomputed from an opaque copy of the lane id inside the loop (`lo`), so the
   // compiler does not hoist ~40 loop-invariant addresses into registers the accumulators need.
-  i32x4 stg[KS];
-  auto load = [&](int tile, int lo) {
+  i32x4 stgA[KS], stgB[KS];
+  auto load = [&](i32x4 (&stg)[KS], int tile, int lo) {
 #pragma unroll
     for (int i = 0; i < KS; ++i) {
       const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
@@ -235,8 +255,9 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
     const int hm = a.head_map[hd];
     if (hm >= 0) pr_row = a.probs + ((long long)row * a.n_align + hm) * a.T;
   }
-  if (tb < te) load(tb, lane);
-  for (int tile = tb; tile < te; ++tile) {
+  // one tile: its staged registers -> the wave's LDS image, the loads of tile + DEPTH into the same
+  // registers, then S^T, the cross-wave sum, the online softmax and U^T
+  auto tile_step = [&](int tile, i32x4 (&stg)[KS]) {
     int lo = lane;
     asm volatile("" : "+v"(lo));
     // wave-private LDS image of this tile (this wave's earlier reads of it are complete: LDS is in order)
@@ -245,7 +266,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
       const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
       *(i32x4*)(sE + r * LDR + 8 * xchunk(r, ch)) = stg[i];
     }
-    if (tile + 1 < te) load(tile + 1, lo);
+    if (tile + DEPTH < te) load(stg, tile + DEPTH, lo);
     // ---- S^T partial over this wave's columns
     f32x16 sc = xzero16();
     {
@@ -332,6 +353,12 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
           o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[ks], o[c], 0, 0, 0);
         }
     }
+  };
+  if (tb < te) load(stgA, tb, lane);
+  if (DEPTH == 2 && tb + 1 < te) load(stgB, tb + 1, lane);
+  for (int tile = tb; tile < te; tile += DEPTH) {
+    tile_step(tile, stgA);
+    if (DEPTH == 2 && tile + 1 < te) tile_step(tile + 1, stgB);
   }
   l_run += __shfl_xor(l_run, 32, 64);
   if (valid) {
@@ -341,7 +368,11 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
       a.part_ml[2 * pi] = m_run;
       a.part_ml[2 * pi + 1] = l_run;
     }
-    bf16* up = a.part_u + pi * a.d + cb + 4 * hh;
+    // u column c = cb + 32 c' + 8 g + 4 hh + e lives in 16-column block c / 16 = cb/16 + 2 c' + (g >> 1) at
+    // position 8 (g & 1) + 4 hh + e; a block holds every row of the slab, so xcomb reads 32 rows x 32 B
+    // contiguously
+    const long long kstride = a.slab_rows * 16;
+    bf16* up = a.part_u + (((long long)split * a.H + hd) * (a.d / 16) + cb / 16) * kstride + (long long)row * 16 + 4 * hh;
 #pragma unroll
     for (int c = 0; c < CT; ++c)
 #pragma unroll
@@ -349,7 +380,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
         bf16x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = f2bf(o[c][4 * g + e] * inv);
-        *(bf16x4*)(up + 32 * c + 8 * g) = w;
+        *(bf16x4*)(up + (2 * c + (g >> 1)) * kstride + 8 * (g & 1)) = w;
       }
   }
 }
@@ -357,7 +388,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 // ------------------------------------------------------------------------------------------------------
 struct XCombArgs {
   const bf16* part_u; const float* part_ml; int splits; long long slab_rows;
-  const bf16* wv; const float* bv;       // this layer's V projection [d][d] (row h*64 + j) and bias [d]
+  const bf16* wvb; const float* bv;      // this layer's V projection packed [H][d/16][64][16], bias [d]
   const int* row_hyp; const int* done;
   bf16* out; long long ldo;
   int rows, H, d, T;
@@ -377,14 +408,16 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
   const int h = blockIdx.y;
   const int r = blockIdx.x * 32 + l32;
-  const bool valid = r < a.rows && !(a.done && a.done[a.row_hyp[r]]);
+  const int rc = min(r, a.rows - 1);
   const long long sstride = a.slab_rows * a.H;          // (row, head) pairs per split slab
   float w[MAXS];
   float Mx = -INFINITY, L = 0.f;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) w[s] = 0.f;
-  if (valid) {
-    const float* ml = a.part_ml + 2 * ((long long)r * a.H + h);
+  {
+    // every load is issued regardless of the row's state (rows past the end clamped; a finished row's
+    // partials are stale but finite, and its output is never stored), so nothing waits on `done`
+    const float* ml = a.part_ml + 2 * ((long long)rc * a.H + h);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
       if (s < a.splits) Mx = fmaxf(Mx, ml[2 * s * sstride]);
@@ -399,22 +432,24 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
     for (int s = 0; s < MAXS; ++s) w[s] *= inv;
   }
   f32x16 acc[2] = {xzero16(), xzero16()};
-  const int cb = wv * (KS8 * 16);
-  const bf16* pu = a.part_u + ((long long)min(r, a.rows - 1) * a.H + h) * a.d + cb + 8 * hh;
-  const bf16* w0 = a.wv + (long long)(h * 64 + l32) * a.d + cb + 8 * hh;
-  const bf16* w1 = w0 + 32LL * a.d;
-  const long long pstride = sstride * a.d;
+  const int kb0 = wv * KS8;               // this wave's first 16-column block
+  const long long kstride = a.slab_rows * 16;
+  const bf16* pu = a.part_u + ((long long)h * (a.d / 16) + kb0) * kstride + (long long)rc * 16 + 8 * hh;
+  const bf16* w0 = a.wvb + (((long long)h * (a.d / 16) + kb0) * 64 + l32) * 16 + 8 * hh;
+  const bf16* w1 = w0 + 32 * 16;
+  const long long pstride = (long long)a.H * a.d * a.slab_rows;   // one split slab
 #pragma unroll
   for (int s0 = 0; s0 < KS8; s0 += KB) {
     bf16x8 pv[KB][MAXS], wa[KB], wb[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       if (s0 + k >= KS8) break;
-      wa[k] = *(const bf16x8*)(w0 + 16 * (s0 + k));
-      wb[k] = *(const bf16x8*)(w1 + 16 * (s0 + k));
+      wa[k] = *(const bf16x8*)(w0 + (s0 + k) * 64 * 16);
+      wb[k] = *(const bf16x8*)(w1 + (s0 + k) * 64 * 16);
 #pragma unroll
       for (int sp = 0; sp < MAXS; ++sp)
-        if (sp < a.splits) pv[k][sp] = *(const bf16x8*)(pu + sp * pstride + 16 * (s0 + k));
+        if (sp < a.splits) pv[k][sp] = *(const bf16x8*)(pu + sp * pstride + (s0 + k) * kstride);
+        else pv[k][sp] = bf16x8{};
     }
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
@@ -474,11 +509,11 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
 // ------------------------------------------------------------------------------------------------------
 // host launchers
 
-void launch_xpack_wkt(const bf16* ckv_w, bf16* wkt, int L, int H, int d, hipStream_t st) {
+void launch_xpack(const bf16* ckv_w, bf16* wkt, bf16* wvb, int L, int H, int d, hipStream_t st) {
   const long long total = (long long)L * H * d * 64;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(xpack_wkt_kernel, dim3(blocks), dim3(256), 0, st, ckv_w, wkt, L, H, d);
-  WM_LAUNCH_CHECK("xpack_wkt_kernel");
+  hipLaunchKernelGGL(xpack_kernel, dim3(blocks), dim3(256), 0, st, ckv_w, wkt, wvb, L, H, d);
+  WM_LAUNCH_CHECK("xpack_kernel");
 }
 
 void launch_xq(const bf16* q, long long ldq, const CrossFuse& fz, const bf16* wkt, bf16* qp, int rows, int H, int d,
@@ -496,8 +531,10 @@ void launch_xq(const bf16* q, long long ldq, const CrossFuse& fz, const bf16* wk
 }
 
 // Key splits of a pass.  A function of the whole pass, so slicing a pass into launches never changes a
-// row's arithmetic: about three rounds of 256 one-workgroup CUs, at most 16, at least one 32-position tile
-// per split, and the bf16 partial slabs capped at 256 MB.
+// row's arithmetic: about 1.75 rounds of 256 one-workgroup CUs (measured on the 150-window large-v3
+// decode: 1 / 2 / 3 / 4 / 5 splits -> 522 / 564 / 450 / 510 / 483 ms of attention per bench step; fewer,
+// longer items amortise each item's prologue and epilogue, more of them fill the last round), at most 16,
+// at least one 32-position tile per split, and the bf16 partial slabs capped at 256 MB.
 int xattn_splits(int plan_rows, int group, int H, int T, int d) {
   static const int forced = [] {
     const char* e = std::getenv("VLOG_AMD_XSPLITS");
@@ -507,7 +544,7 @@ int xattn_splits(int plan_rows, int group, int H, int T, int d) {
   const long long n_mt = ((long long)group * H + 31) / 32;
   const long long items = groups * n_mt;
   const int n_tiles = (T + 31) / 32;
-  int s = (int)((768 + items / 2) / items);
+  int s = (int)((448 + items / 2) / items);
   if (forced > 0) s = forced;
   s = std::max(1, std::min(s, std::min(XMAXS, n_tiles)));
   const long long slab = (long long)plan_rows * H * d * 2;
@@ -532,27 +569,34 @@ void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const in
   a.slab_rows = slab_rows; a.part_u = part_u; a.part_ml = part_ml;
   a.probs = probs; a.head_map = head_map; a.n_align = n_align; a.stat = stat;
   const dim3 grid(a.per_xcd * 8);
-#define XA_LAUNCH(QW_, NW_)                                                                                \
-  if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a);   \
-  else hipLaunchKernelGGL((xattn_kernel<QW_, NW_>), grid, dim3(NW_ * 64), 0, st, a);
-  switch (d) {                           // 8 waves of d/8 columns (registers: no spills), 4 for tiny
-    case 384: XA_LAUNCH(96, 4); break;
-    case 512: XA_LAUNCH(64, 8); break;
-    case 768: XA_LAUNCH(96, 8); break;
-    case 1024: XA_LAUNCH(128, 8); break;
-    case 1280: XA_LAUNCH(160, 8); break;
+  static const int form = [] {
+    const char* e = std::getenv("VLOG_AMD_XFORM");
+    return e ? std::atoi(e) : 0;
+  }();
+#define XA_LAUNCH(QW_, NW_, DP_)                                                                                \
+  if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a);   \
+  else hipLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_>), grid, dim3(NW_ * 64), 0, st, a);
+  // form 0 (default): 8 waves x d/8 columns, one tile staged ahead (80 KB of E in flight per CU);
+  // form 1 (VLOG_AMD_XFORM=1, experiment): 4 waves x d/4 columns, two tiles ahead (160 KB), which needs
+  // more than the 256 architectural VGPRs per lane at d >= 1024 (spills)
+  switch (d) {
+    case 384: if (form) { XA_LAUNCH(96, 4, 2); } else { XA_LAUNCH(96, 4, 1); } break;
+    case 512: if (form) { XA_LAUNCH(128, 4, 2); } else { XA_LAUNCH(64, 8, 1); } break;
+    case 768: if (form) { XA_LAUNCH(192, 4, 2); } else { XA_LAUNCH(96, 8, 1); } break;
+    case 1024: if (form) { XA_LAUNCH(256, 4, 2); } else { XA_LAUNCH(128, 8, 1); } break;
+    case 1280: if (form) { XA_LAUNCH(320, 4, 2); } else { XA_LAUNCH(160, 8, 1); } break;
     default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
   }
 #undef XA_LAUNCH
   WM_LAUNCH_CHECK("xattn_kernel");
 }
 
-void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long long slab_rows, const bf16* wv,
+void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long long slab_rows, const bf16* wvb,
                      const float* bv, const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H,
                      int d, int T, float* probs, const int* head_map, int n_align, hipStream_t st) {
   if (rows <= 0) return;
   XCombArgs a{};
-  a.part_u = part_u; a.part_ml = part_ml; a.splits = splits; a.slab_rows = slab_rows; a.wv = wv; a.bv = bv;
+  a.part_u = part_u; a.part_ml = part_ml; a.splits = splits; a.slab_rows = slab_rows; a.wvb = wvb; a.bv = bv;
   a.row_hyp = row_hyp; a.done = done; a.out = out; a.ldo = ldo; a.rows = rows; a.H = H; a.d = d; a.T = T;
   a.probs = probs; a.head_map = head_map; a.n_align = n_align;
   const dim3 grid((rows + 31) / 32, H);
@@ -560,6 +604,7 @@ void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long 
   if (splits <= 1) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 1>), grid, dim3(512), 0, st, a);             \
   else if (splits <= 2) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 2>), grid, dim3(512), 0, st, a);        \
   else if (splits <= 4) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 4>), grid, dim3(512), 0, st, a);        \
+  else if (splits <= 8) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 8>), grid, dim3(512), 0, st, a);        \
   else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, XMAXS>), grid, dim3(512), 0, st, a);
   switch (d) {                           // 8 waves x d/8 columns of the reduction: d/128 k-steps each
     case 384: XC_LAUNCH(3); break;

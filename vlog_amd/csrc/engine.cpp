@@ -41,7 +41,7 @@ void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, co
                        const CrossFuse&, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 
 // factored cross-attention over the encoder output (attn_xenc.hip)
-void launch_xpack_wkt(const bf16*, bf16*, int, int, int, hipStream_t);
+void launch_xpack(const bf16*, bf16*, bf16*, int, int, int, hipStream_t);
 void launch_xq(const bf16*, long long, const CrossFuse&, const bf16*, bf16*, int, int, int, hipStream_t);
 int xattn_splits(int, int, int, int, int);
 void launch_xattn(const bf16*, const bf16*, const int*, const int*, const int*, int, long long, int, int, int, int, int,
@@ -147,6 +147,7 @@ struct wm_engine {
   int cross_mode = 1;
   DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs
   DevBuf xwkt;               // factored: Wk^T per layer and head [L][H][d][64] bf16, packed from dec.ckv.w
+  DevBuf xwvb;               // factored: Wv per layer and head in 16-column blocks [L][H][d/16][64][16]
   bool xwkt_ready = false;
   DevBuf s_qp, s_pu, s_pml;  // factored step scratch: q' [rows][H][d], split partials u/l and (m, l)
   int cross_cap = 0;         // cross-attention grid cap (0: one block per item; >0: persistent grid-stride form,
@@ -179,7 +180,7 @@ struct wm_engine {
 
   size_t device_bytes() const {
     size_t t = arena.bytes;
-    for (const DevBuf* b : {&e_cols, &e_h1, &e_x, &e_hb, &e_qkv, &e_ao, &e_ff, &ckv, &xenc, &xwkt, &s_qp, &s_pu, &skv, &s_x, &s_hb, &s_q, &s_ao,
+    for (const DevBuf* b : {&e_cols, &e_h1, &e_x, &e_hb, &e_qkv, &e_ao, &e_ff, &ckv, &xenc, &xwkt, &xwvb, &s_qp, &s_pu, &skv, &s_x, &s_hb, &s_q, &s_ao,
                             &s_ff, &s_logits, &s_pm, &s_pl, &s_po, &d_tokens, &d_lin, &d_fin_tok})
       t += b->bytes;
     return t;
@@ -532,10 +533,10 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     const int splits = xattn_splits(sl.total_rows, cross_group, H, T, d);
     const size_t prow = (size_t)H * d;
     bf16* qp = e->s_qp.as<bf16>() + (size_t)r0 * prow;
-    bf16* pu = e->s_pu.as<bf16>() + (size_t)r0 * prow;
+    bf16* pu = e->s_pu.as<bf16>() + (size_t)r0 * 16;         // blocked layout: rows are 16-element records
     float* pml = e->s_pml.as<float>() + (size_t)r0 * H * 2;
     const bf16* wkt = e->xwkt.as<bf16>() + (size_t)l * H * d * 64;
-    const bf16* wv = e->Wb("dec.ckv.w") + ((size_t)l * 2 * d + d) * d;
+    const bf16* wv = e->xwvb.as<bf16>() + (size_t)l * H * d * 64;
     const float* bv = e->Wf("dec.ckv.b") + (size_t)l * 2 * d + d;
     {
       ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * H * d * 64, 2.0 * H * d * 64 + 2.0 * rows * d + 2.0 * rows * prow);
@@ -603,7 +604,8 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
     e->s_pml.ensure((size_t)splits * rows * H * 2 * 4);
     if (!e->xwkt_ready) {
       e->xwkt.ensure((size_t)L * H * d * 64 * 2);
-      launch_xpack_wkt(e->Wb("dec.ckv.w"), e->xwkt.as<bf16>(), L, H, d, st);
+      e->xwvb.ensure((size_t)L * H * d * 64 * 2);
+      launch_xpack(e->Wb("dec.ckv.w"), e->xwkt.as<bf16>(), e->xwvb.as<bf16>(), L, H, d, st);
       e->xwkt_ready = true;
     }
     if (!e->xenc.p) throw std::runtime_error("decoder: no encoder slots (wm_reserve + wm_cross_kv first)");
@@ -1035,7 +1037,7 @@ void wm_destroy(wm_engine* e) {
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
                     &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt,
-                    &e->xenc, &e->xwkt, &e->s_qp, &e->s_pu, &e->s_pml})
+                    &e->xenc, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml})
     b->release();
   if (e->st2) (void)hipStreamDestroy(e->st2);
   for (hipEvent_t ev : {e->ev_fork, e->ev_mid, e->ev_join})
