@@ -62,11 +62,14 @@ int wm_frame_energy(wm_engine* e, const float* d_pcm, int64_t n_samples, int32_t
 int wm_encode(wm_engine* e, const float* d_mel, int64_t ld, const int32_t* h_seek, const int32_t* h_nframes,
               int32_t B, void* d_enc_out, void* stream);
 
-/* Capacity of the decoder state: n_slots windows of cross-KV, n_hyp hypotheses of self-KV. */
+/* Capacity of the decoder state: n_slots windows (encoder outputs, or cross-KV panels with cross_mode 0),
+ * n_hyp hypotheses of self-KV. */
 int wm_reserve(wm_engine* e, int32_t n_slots, int32_t n_hyp, void* stream);
 
-/* Cross-attention K/V projection of B encoder outputs into slots [slot0, slot0+B) (all decoder layers;
- * CTranslate2 computes these inside generate [FW↑]). */
+/* Makes B encoder outputs the cross-attention memory of slots [slot0, slot0+B) (CTranslate2 projects them
+ * to K/V inside generate [FW↑]).  Default (factored cross-attention): the slot keeps the encoder output
+ * itself and the decoder attends over it (q' = Wk_h^T q, u = P E, Wv after the merge).  cross_mode 0: the
+ * K/V projection of all decoder layers is computed here. */
 int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void* stream);
 
 /* ctranslate2 Whisper.generate(encoder_output, prompts, ...) [FW↑] as faster-whisper
@@ -140,6 +143,9 @@ int32_t wm_profile_classes(void);
 const char* wm_profile_name(int32_t cls);
 int wm_profile(wm_engine* e, int32_t enable);
 /* Engine options (no reference counterpart: scheduling knobs of this build only).
+ *   "cross_mode" (default 1): 1 = factored cross-attention over the encoder output (attn_xenc.hip),
+ *   0 = projected cross-KV panels (attn_dec.hip).  Switching re-allocates the window slots (their content is
+ *   dropped: call wm_cross_kv again).  The two forms agree to bf16 rounding (not bit-identical).
  *   "decode_split" (default 0): decode steps with >= 32 rows run as two row slices on two streams, one
  *   slice's weight GEMMs overlapping the other's cross-attention.  Results are bit-identical
  *   either way; off by default because the overlap measured slower on MI355X (the GEMM blocks queue behind
@@ -150,7 +156,7 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its
  *   (window, head, key split) items with a grid stride; 0 launches one block per item.
  *   "cross_attn_fuse" (default 1): bit 0 folds the cq projection's split-K combine into the cross-attention
- *   kernel's q load; bit 1 combines the key splits in-kernel (last-arriving split) instead of a combine
+ *   kernel's q load (the q' kernel's, in the factored form); bit 1 combines the key splits in-kernel (last-arriving split) instead of a combine
  *   launch.  Every setting of these three knobs gives bit-identical results.
  *   "encode_chunk" (default 160): windows per encoder pass inside wm_encode (~52 MB of activation scratch
  *   per large-v3 window). */

@@ -151,20 +151,59 @@ def test_alignment_postprocess_matches_oracle(setup):
     assert len(jg) == len(jr) and np.mean(jg == jr) >= 0.97
 
 
-def test_word_alignment_end_to_end_vs_oracle(setup):
-    """Whole align (bf16 decoder) vs the float32 oracle.  The synthetic model's cross-attention is nearly
-    uniform, so DTW near-ties can move the path tail; the bar is 90 % of token start times within 20 ms."""
-    dims, eng, orc, encf, W = setup
+def _align_vs_oracle(eng, orc, encf, dims, slot):
     st = dims.specials
     tok = Tokenizer(dims, language="en")
     text = list(range(1000, 1040))
     heads = dims.default_alignment_heads()
-    probs, ti, tj = eng.align(3, tok.sot_sequence, text, 3000, heads, 7)
-    rp, ri, rj = find_alignment(orc, orc.cross_kv(encf[3:4]), tok.sot_sequence, text, st, 3000, heads)
+    probs, ti, tj = eng.align(slot, tok.sot_sequence, text, 3000, heads, 7)
+    rp, ri, rj = find_alignment(orc, orc.cross_kv(encf[slot:slot + 1]), tok.sot_sequence, text, st, 3000, heads)
     assert np.allclose(probs, rp, rtol=0.05, atol=1e-6)
     jg, jr = _jumps(ti, tj), _jumps(ri, rj)
     assert len(jg) == len(jr)
-    assert np.mean(np.abs(jg - jr) <= 1) >= 0.90
+    return float(np.mean(np.abs(jg - jr) <= 1))
+
+
+def test_word_alignment_end_to_end_vs_oracle(setup):
+    """Whole align (bf16 decoder) vs the float32 oracle on the synthetic model.  Its cross-attention is nearly
+    uniform, so DTW near-ties move the path tail under any bf16 noise: the projected (cross_mode 0) and the
+    factored form (default) carry score errors of the same size and land at 0.85-0.93 of
+    token start times within 20 ms depending on the noise draw; this checks both stay in that band.  The
+    well-conditioned bar is the sharpened-attention test below."""
+    dims, eng, orc, encf, W = setup
+    enc = torch.from_numpy(encf).to(torch.bfloat16).cuda()
+    frac = {}
+    for mode in (0, 1):
+        eng.set_option("cross_mode", mode)
+        eng.cross_kv(enc, 0)
+        frac[mode] = _align_vs_oracle(eng, orc, encf, dims, 3)
+    assert min(frac.values()) >= 0.80, frac
+
+
+def test_word_alignment_sharpened_attention_vs_oracle():
+    """The same end-to-end alignment on a model whose alignment-layer cross-attention queries are scaled by 6
+    (peaked attention, as a trained model's alignment heads): fewer DTW near-ties, so a tighter bar — >= 90 %
+    of token start times within 20 ms of the oracle in both cross-attention forms, per window."""
+    from vlog_amd.engine import GpuEngine
+    dims = model_dims("tiny")
+    sd = synthetic_state_dict(dims, seed=3, eot_after=60)
+    for l in sorted({l for l, _ in dims.default_alignment_heads()}):
+        p = f"model.decoder.layers.{l}.encoder_attn.q_proj."
+        sd[p + "weight"] = sd[p + "weight"] * 6.0
+        sd[p + "bias"] = sd[p + "bias"] * 6.0
+    eng = GpuEngine(dims, sd, 0)
+    orc = OracleWhisper(round_bf16(sd), dims, np.float32)
+    x = np.concatenate([speech_like(30.0, 200 + i) for i in range(2)])
+    feats = omel.log_mel(x, dims.n_mels)
+    enc = eng.encode(torch.from_numpy(feats).cuda(), [0, 3000], [3000, 3000])
+    eng.reserve(2, 4)
+    encf = enc.float().cpu().numpy()
+    frac = {}
+    for mode in (0, 1):
+        eng.set_option("cross_mode", mode)
+        eng.cross_kv(enc, 0)
+        frac[mode] = [_align_vs_oracle(eng, orc, encf, dims, slot) for slot in (0, 1)]
+    assert min(min(v) for v in frac.values()) >= 0.90, frac
 
 
 class _GpuBackend:
