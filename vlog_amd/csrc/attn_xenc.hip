@@ -29,7 +29,9 @@
 //                                   come from the same LDS image through ds_read_b64_tr_b16).
 //                   E is streamed with coalesced 16-B non-temporal loads, register-staged one tile ahead,
 //                   into a wave-private LDS image, so no barrier guards it.  Output per split: (m, l) and
-//                   u / l as bf16.
+//                   u / l as bf16.  (Tried: each wave streaming whole contiguous rows into a block-shared
+//                   image reads faster alone, 5.1-5.5 vs 4.7-4.8 TB/s loads-only in tools/xattn_bench, but
+//                   the two extra barriers per tile cost more than that with the compute in: 3181 vs 3217.)
 //   xcomb_vo_kernel merges the key splits (weights l_s 2^(m_s - M) / L) and applies Wv_h and bv_h (MFMA,
 //                   K = d) -> the attention output ao [rows][d].  With capture on, it also turns the raw
 //                   scores that xattn wrote for the alignment heads into probabilities.
@@ -184,6 +186,8 @@ struct XAttnArgs {
   float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
   float* probs; const int* head_map; int n_align;   // capture: raw scores [row][n_align][T]
   unsigned long long* stat;
+  int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0): bit 0 skips
+                                         // the S MFMAs, bit 1 the cross-wave sum, bit 2 the U phase
 };
 
 template <int QW, int NW, int DEPTH>
@@ -274,29 +278,33 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
       const int l32o = lo & 31, g = (l32o >> 2) & 3;
       const bf16* s0 = sE + l32o * LDR + 8 * (hh ^ g);
       const bf16* s1 = sE + l32o * LDR + 8 * ((2 + hh) ^ g);
+      if (!(a.abl & 1)) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 ea = *(const bf16x8*)(((s & 1) ? s1 : s0) + 32 * (s >> 1));
-        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ea, qf[s], sc, 0, 0, 0);
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8 ea = *(const bf16x8*)(((s & 1) ? s1 : s0) + 32 * (s >> 1));
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ea, qf[s], sc, 0, 0, 0);
+        }
       }
     }
     // the NW partials -> the full S^T in every wave: partials to LDS; wave w sums registers
     // [w RPW, (w+1) RPW) over the waves in a fixed order (0..NW-1); every wave reads the 16 sums back
     constexpr int RPW = 16 / NW;
+    if (!(a.abl & 2)) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sX[(wv * 16 + r) * 64 + lane] = sc[r];
-    __syncthreads();
+      for (int r = 0; r < 16; ++r) sX[(wv * 16 + r) * 64 + lane] = sc[r];
+      __syncthreads();
 #pragma unroll
-    for (int k = 0; k < RPW; ++k) {
-      const int r = wv * RPW + k;
-      float v = sX[r * 64 + lane];
+      for (int k = 0; k < RPW; ++k) {
+        const int r = wv * RPW + k;
+        float v = sX[r * 64 + lane];
 #pragma unroll
-      for (int w2 = 1; w2 < NW; ++w2) v += sX[(w2 * 16 + r) * 64 + lane];
-      sRed[r * 64 + lane] = v;
+        for (int w2 = 1; w2 < NW; ++w2) v += sX[(w2 * 16 + r) * 64 + lane];
+        sRed[r * 64 + lane] = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = sRed[r * 64 + lane];
     }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sc[r] = sRed[r * 64 + lane];
     const int t0 = tile * 32;
     if (t0 + 32 > a.T) {
 #pragma unroll
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
     // ---- U^T (wave cols) += E^T . P^T.  Transposed read of rows 16 ks + 8 jh + 4 hh + gq, columns
     // 32 c + 16 (G4 & 1) + 4 gp: chunk 4 c + lowc (lowc = 2 (G4 & 1) + (gp >> 1)) is stored at
     // 4 c + (lowc ^ (2 jh + hh)), so each jh has one base address and (ks, c) are immediate offsets.
-    {
+    if (!(a.abl & 4)) {
       const int G4 = (lo >> 4) & 3, gi = lo & 15, gq = gi >> 2, gp = gi & 3;
       const int lowc = 2 * (G4 & 1) + (gp >> 1);
       const bf16* tb0 = sE + (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
@@ -552,6 +560,9 @@ int xattn_splits(int plan_rows, int group, int H, int T, int d) {
   return s;
 }
 
+static int g_xattn_abl = 0;
+void xattn_set_ablation(int abl) { g_xattn_abl = abl; }
+
 void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const int* row_hyp, const int* done, int rows,
                   long long slab_rows, int group, int H, int T, int d, int splits, bf16* part_u, float* part_ml,
                   float* probs, const int* head_map, int n_align, unsigned long long* stat, hipStream_t st,
@@ -567,7 +578,7 @@ void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const in
   a.n_items = (int)items;
   a.per_xcd = (a.n_items + 7) / 8;
   a.slab_rows = slab_rows; a.part_u = part_u; a.part_ml = part_ml;
-  a.probs = probs; a.head_map = head_map; a.n_align = n_align; a.stat = stat;
+  a.probs = probs; a.head_map = head_map; a.n_align = n_align; a.stat = stat; a.abl = g_xattn_abl;
   const dim3 grid(a.per_xcd * 8);
   static const int form = [] {
     const char* e = std::getenv("VLOG_AMD_XFORM");
