@@ -33,9 +33,9 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double bytes = (double)W * T * d * 2;
-  for (int abl : {0, 7}) {
+  for (int abl : {0, 7, 8, 15}) {
     xattn_set_ablation(abl);
-    for (int splits : {1, 2, 3, 4, 5}) {
+    for (int splits : {1, 3, 5}) {
       for (int i = 0; i < 3; ++i)
         launch_xattn(qp, enc, slot, rh, nullptr, W, W, 1, H, T, d, splits, pu, pml, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr);
       CK(hipEventRecord(e0, 0));

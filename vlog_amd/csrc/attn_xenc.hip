@@ -187,7 +187,9 @@ struct XAttnArgs {
   float* probs; const int* head_map; int n_align;   // capture: raw scores [row][n_align][T]
   unsigned long long* stat;
   int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0): bit 0 skips
-                                         // the S MFMAs, bit 1 the cross-wave sum, bit 2 the U phase
+                                         // the S MFMAs, bit 1 the cross-wave sum, bit 2 the U phase, bit 3
+                                         // loads E with plain loads (same-box bench: 1 % slower than
+                                         // non-temporal ones; tools/gpu_ablib.sh)
 };
 
 template <int QW, int NW, int DEPTH>
@@ -251,7 +253,8 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
     for (int i = 0; i < KS; ++i) {
       const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
       const int t = min(tile * 32 + r, a.T - 1);
-      stg[i] = __builtin_nontemporal_load((const i32x4*)(E + (long long)t * a.d + ch * 8));
+      if (a.abl & 8) stg[i] = *(const i32x4*)(E + (long long)t * a.d + ch * 8);
+      else stg[i] = __builtin_nontemporal_load((const i32x4*)(E + (long long)t * a.d + ch * 8));
     }
   };
   float* pr_row = nullptr;
@@ -560,7 +563,10 @@ int xattn_splits(int plan_rows, int group, int H, int T, int d) {
   return s;
 }
 
-static int g_xattn_abl = 0;
+static int g_xattn_abl = [] {            // ablation / load-policy experiments (VLOG_AMD_XABL); product: 0
+  const char* e = std::getenv("VLOG_AMD_XABL");
+  return e ? std::atoi(e) : 0;
+}();
 void xattn_set_ablation(int abl) { g_xattn_abl = abl; }
 
 void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const int* row_hyp, const int* done, int rows,
