@@ -55,8 +55,10 @@ def build_shard(rank: int, W: int):
 
 
 class Pipeline:
-    def __init__(self, eng, tok, dims, rank, world, W, beam, pcm_dev, margin_left, n_total):
+    def __init__(self, eng, tok, dims, rank, world, W, beam, pcm_dev, margin_left, n_total, host_group=None):
         self.eng, self.tok, self.dims = eng, tok, dims
+        self.host_group = host_group
+        self.keep_windows = ()                  # windows whose encoder output the next step copies to the host
         self.rank, self.world, self.W, self.beam = rank, world, W, beam
         self.pcm_dev, self.margin_left, self.n_total = pcm_dev, margin_left, n_total
         st = dims.specials
@@ -70,13 +72,15 @@ class Pipeline:
         frame0 = self.rank * W * 3000
         mel, gmax = eng.logmel(self.pcm_dev, n_samples=self.n_total, pcm_offset=frame0 * 160 - self.margin_left,
                                frame0=frame0, n_frames=W * 3000)
-        g = torch.tensor([eng.gmax_value(gmax)], dtype=torch.float32)
         if self.world > 1:
+            # faster-whisper's clamp uses the WHOLE file's log-mel max: the one cross-shard value, exchanged
+            # as a host float over a gloo group (no RCCL collective on the data path)
             import torch.distributed as dist
-            gd = g.to(eng.device)
-            dist.all_reduce(gd, op=dist.ReduceOp.MAX)
-            g = gd.cpu()
-        eng.logmel_finalize(mel, gmax, float(g[0]))
+            g = torch.tensor([eng.gmax_value(gmax)], dtype=torch.float32)
+            dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.host_group)
+            eng.logmel_finalize(mel, gmax, float(g[0]))
+        else:
+            eng.logmel_finalize(mel, gmax)          # single shard: the clamp reads the max on the device
         t1 = time.perf_counter()
         enc = eng.encode(mel, [i * 3000 for i in range(W)], [3000] * W)
         eng.cross_kv(enc, 0)
@@ -99,7 +103,90 @@ class Pipeline:
         for k, v in (("logmel", t1 - t0), ("encode", t2 - t1), ("decode", t3 - t2), ("host", t4 - t3)):
             self.stage[k] = self.stage.get(k, 0.0) + v
         self.last = dict(tokens=[len(r.tokens) for r in res], steps=steps, segments=len(segs), vtt_bytes=len(vtt))
+        if self.keep_windows:
+            self.kept = dict(res=res, enc={w: enc[w].float().cpu().numpy() for w in self.keep_windows})
         del enc, mel
+
+
+def host_cpu() -> dict:
+    """lscpu model name and physical core count of this host (the CPU baseline states both)."""
+    info = {"model": None, "physical_cores": None, "logical_cpus": os.cpu_count()}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {}
+        for line in out.splitlines():
+            if ":" in line:
+                k, v = line.split(":", 1)
+                kv[k.strip()] = v.strip()
+        info["model"] = kv.get("Model name")
+        if kv.get("Core(s) per socket") and kv.get("Socket(s)"):
+            info["physical_cores"] = int(kv["Core(s) per socket"]) * int(kv["Socket(s)"])
+    except Exception:
+        pass
+    if info["model"] is None and os.path.isfile("/proc/cpuinfo"):
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    return info
+
+
+def composite_roofline(dims, lengths, steps: int, prompt_len: int, elapsed_per_step: float, windows: int) -> dict:
+    """SURVEY.md §8(d) composite bound for one step: encoder FLOPs at the dense bf16 MFMA peak plus decoder bytes at
+    the HBM peak, over the measured step time, using the ACTUAL generated length of every window.  Two byte
+    accountings: `factored` (what this engine streams: each active window's encoder output, L x 1500 x d bf16,
+    per decoder step) and `projected` (§8(d) as written: L x 2 x 1500 x d bf16 of cross-K/V per window-step,
+    plus the K/V projection FLOPs)."""
+    L, d, T = dims.n_dec_layer, dims.n_state, dims.n_audio_ctx
+    win_steps = sum(n + 1 for n in lengths)                        # token-producing steps per window (incl. eot)
+    pos_sum = sum(sum(prompt_len + s for s in range(n + 1)) for n in lengths)
+    w_bytes = dims.decoder_weight_bytes() * steps
+    self_kv = dims.self_kv_bytes_per_position() * pos_sum
+    enc_fl = dims.encoder_flops_per_window() * windows
+    out = {}
+    for name, xbytes, xfl in (("factored", L * T * d * 2.0, 0.0),
+                              ("projected", dims.cross_kv_bytes_per_window(), dims.cross_kv_flops_per_window())):
+        t_mfma = (enc_fl + xfl * windows) / (MFMA_BF16_PEAK_TFS * 1e12)
+        t_hbm = (w_bytes + self_kv + xbytes * win_steps) / (HBM_PEAK_GBS * 1e9)
+        out[name] = {"t_ideal_ms": round(1e3 * (t_mfma + t_hbm), 2), "mfma_ms": round(1e3 * t_mfma, 2),
+                     "hbm_ms": round(1e3 * t_hbm, 2), "frac": round((t_mfma + t_hbm) / elapsed_per_step, 4)}
+    return out
+
+
+def parity_sample(dims, sd, pipe, n_sample: int = 8) -> dict:
+    """Outside the timed region: sampled windows of the last step, decoded by the CPU oracle (engine numeric
+    format) from the GPU's own encoder output.  A window is identical when every GPU token is the oracle's
+    argmax (teacher-forced, tests/parity_util.py); non-identical windows are re-decoded by the oracle's greedy
+    search for the WER of the GPU text against the oracle text (no ground truth exists for synthetic audio, so
+    this WER bounds the WER delta)."""
+    sys.path.insert(0, ROOT)
+    from oracle.decode import GenerateOptions, generate_one
+    from oracle.model import OracleWhisper
+    from tests.parity_util import sample_indices, window_parity
+    from vlog_amd.metrics import word_error_rate
+    from vlog_amd.weights import round_bf16
+
+    orc = OracleWhisper(round_bf16(sd), dims, np.float32, bf16_acts=True)
+    res, enc = pipe.kept["res"], pipe.kept["enc"]
+    opt = GenerateOptions(suppress_tokens=pipe.suppress, max_length=448)
+    ident, margins, ref_txt, hyp_txt = 0, [], [], []
+    for w in sorted(enc):
+        r = window_parity(orc, enc[w], pipe.prompt, res[w], dims.specials, opt, w)
+        ident += r.identical
+        margins.append(r.min_margin)
+        hyp_txt.append(pipe.tok.decode(res[w].tokens))
+        if r.identical:
+            ref_txt.append(hyp_txt[-1])
+        else:
+            o = generate_one(orc, orc.cross_kv(enc[w][None]), pipe.prompt, dims.specials, opt)
+            ref_txt.append(pipe.tok.decode(o.tokens))
+    wer = word_error_rate(" ".join(ref_txt), " ".join(hyp_txt))
+    return {"n": len(enc), "windows_identical": ident, "windows": sorted(enc), "wer_delta": round(wer, 5),
+            "min_margin_nats": round(min(margins), 5),
+            "method": "GPU tokens teacher-forced through oracle/ (bf16-activation mode) on the GPU's encoder output; "
+                      "identical = GPU token is the oracle argmax at every step; wer_delta = WER of the GPU text vs "
+                      "the oracle's greedy text over the sampled windows"}
 
 
 def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
@@ -126,7 +213,9 @@ def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
     per_step = (t2 - t1) / n_steps
     per_window = (t1 - t0) + per_step * max(mean_tokens, 1.0)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    hc = host_cpu()
     return {"value": round(30.0 / per_window, 4), "unit": "audio_s/s", "cores": threads, "kind": "port",
+            "cpu_model": hc["model"], "host_physical_cores": hc["physical_cores"], "host_logical_cpus": hc["logical_cpus"],
             "sample": (f"oracle/ numpy fp32 CPU restatement, {dims.name}: one 30 s window log-mel+encoder+cross-KV "
                        f"({t1 - t0:.1f} s) + {n_steps} greedy decoder steps ({per_step:.3f} s/step), extrapolated to "
                        f"{mean_tokens:.1f} tokens/window; faster-whisper CPU baseline unavailable (not installed)")}
@@ -144,22 +233,27 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-kernel event timing")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity sample (rank 0, untimed)")
+    ap.add_argument("--parity-windows", type=int, default=8)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    host_group = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        host_group = dist.new_group(backend="gloo")      # host scalars (log-mel max, timing): no RCCL on the data path
 
     dims = model_dims(args.model)
     t = time.perf_counter()
     sd = synthetic_state_dict(dims, seed=0, eot_after=args.eot_after)
     from vlog_amd.engine import GpuEngine
     eng = GpuEngine(dims, sd, local)
-    if not (rank == 0 and world == 1 and not args.no_cpu_baseline):
+    keep_sd = rank == 0 and ((world == 1 and not args.no_cpu_baseline) or not args.no_parity)
+    if not keep_sd:
         del sd
         sd = None
     tok = Tokenizer(dims, language="en")
@@ -169,7 +263,7 @@ def main():
     n_total = world * W * CLIP
     eng.reserve(W, W * max(1, args.beam))
     log(f"[rank {rank}] setup {time.perf_counter() - t:.1f} s, engine {eng.device_bytes() / 2**30:.1f} GiB")
-    pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total)
+    pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total, host_group)
 
     def barrier():
         torch.cuda.synchronize(eng.device)
@@ -207,9 +301,19 @@ def main():
         prof = eng.profile_read()
     if world > 1:
         import torch.distributed as dist
-        te = torch.tensor([elapsed], device=eng.device, dtype=torch.float64)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        te = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX, group=host_group)
         elapsed = float(te.item())
+    stage_timed = dict(pipe.stage)
+    parity = None
+    if rank == 0 and not args.no_parity and sd is not None and args.beam == 1:
+        from tests.parity_util import sample_indices
+        pipe.keep_windows = tuple(sample_indices(W, args.parity_windows))
+        pipe.step()                                             # untimed: keeps the sampled windows' encoder output
+        try:
+            parity = parity_sample(dims, sd, pipe)
+        except Exception as e:  # reported, never fatal to the GPU measurement
+            parity = {"error": str(e)[:300]}
     audio_s = world * W * 30.0 * args.steps
     value = audio_s / elapsed
     if rank != 0:
@@ -228,7 +332,7 @@ def main():
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
                    "parallelism": f"window-shard x{world}", "weights": f"synthetic seed 0, eot_after={args.eot_after}"},
-        "stages_s_per_step": {k: round(v / args.steps, 4) for k, v in pipe.stage.items()},
+        "stages_s_per_step": {k: round(v / args.steps, 4) for k, v in stage_timed.items()},
     }
     if prof:
         kern = {}
@@ -258,6 +362,8 @@ def main():
                 roof["traffic"] = tj.get(dom)
             except Exception:
                 pass
+        roof["accounting"] = ("factored cross-attention: algorithmic bytes = each active window's encoder output "
+                              "(L x 1500 x d bf16) + q' per launch, counted in-kernel")
         out["roofline"] = roof
         enc_ms = sum(breakdown[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
         enc_fl = sum(breakdown[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
@@ -266,6 +372,12 @@ def main():
         cx = breakdown["cross_attn"]
         out["decoder_kv_read"] = {"achieved_gbs": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6, 1),
                                   "frac_of_8000": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6 / HBM_PEAK_GBS, 4)}
+    comp = composite_roofline(dims, toks, pipe.last["steps"], len(pipe.prompt), elapsed / args.steps, W)
+    out.setdefault("roofline", {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                                "traffic": None})
+    out["roofline"]["composite"] = comp
+    if parity is not None:
+        out["parity"] = parity
     if world == 1 and not args.no_cpu_baseline and sd is not None:
         try:
             out["cpu_baseline"] = cpu_baseline(dims, sd, mean_tok)

@@ -25,10 +25,10 @@ from scipy.special import erf
 def to_bf16(x: np.ndarray) -> np.ndarray:
     """Round float32 values to bfloat16 (round-to-nearest-even) and return them as float32."""
     x32 = np.ascontiguousarray(x, dtype=np.float32)
-    u = x32.view(np.uint32).astype(np.uint64)
-    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
-    out = r.astype(np.uint32).view(np.float32)
-    return np.where(np.isfinite(x32), out, x32).astype(np.float32)
+    u = x32.view(np.uint32)
+    # finite values: u <= 0xFF7FFFFF, so u + 0x8000 cannot wrap in uint32
+    r = ((u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) & np.uint32(0xFFFF0000)).view(np.float32)
+    return np.where(np.isfinite(x32), r, x32)
 
 
 def gelu(x: np.ndarray) -> np.ndarray:
@@ -72,9 +72,11 @@ class OracleWhisper:
     outputs, GELU outputs, cross K/V), with float32 accumulation everywhere else — so a token-identity test
     compares the same arithmetic up to summation order instead of bf16 vs f32 rounding."""
 
-    def __init__(self, sd: Dict[str, np.ndarray], dims, dtype=np.float32, bf16_acts: bool = False):
+    def __init__(self, sd: Dict[str, np.ndarray], dims, dtype=np.float32, bf16_acts: bool = False,
+                 bf16_enc: bool = False):
         self.dims = dims
         self.bf16 = bf16_acts
+        self.bf16_enc = bf16_enc
         self.dtype = dtype
         self.w = {k: np.asarray(v, dtype=dtype) for k, v in sd.items()}
         self.H = dims.n_head
@@ -109,6 +111,8 @@ class OracleWhisper:
     # ---------------------------------------------------------------- encoder
     def encode(self, mel: np.ndarray) -> np.ndarray:
         """mel [B, n_mels, 3000] -> [B, 1500, d]."""
+        if self.bf16_enc:
+            return self._encode_bf16(mel)
         w = self.w
         x = np.asarray(mel, dtype=self.dtype)
         x = gelu(conv1d(x, w["model.encoder.conv1.weight"], w["model.encoder.conv1.bias"], 1))
@@ -125,6 +129,38 @@ class OracleWhisper:
             h = layer_norm(x, w[p + "final_layer_norm.weight"], w[p + "final_layer_norm.bias"])
             x = x + self._lin(gelu(self._lin(h, p + "fc1")), p + "fc2")
         return layer_norm(x, w["model.encoder.layer_norm.weight"], w["model.encoder.layer_norm.bias"])
+
+    def _attn_enc_bf16(self, q, k, v):
+        """Encoder self-attention in the engine's numeric format (libwhisper_mi355 attn_enc_v2_kernel): Q
+        pre-scaled by 1/sqrt(64)*log2(e) and rounded to bf16, S = Q K^T in f32, P = exp2(S - rowmax) rounded to
+        bf16 for the P.V product, the normaliser summed from the unrounded P, output rounded to bf16."""
+        qs = to_bf16(q * np.float32(0.125 * 1.4426950408889634))
+        s = qs @ k.transpose(0, 1, 3, 2)
+        p = np.exp2(s - s.max(-1, keepdims=True))
+        l = p.sum(-1, keepdims=True)
+        return to_bf16((to_bf16(p) @ v) / l)
+
+    def _encode_bf16(self, mel: np.ndarray) -> np.ndarray:
+        """The encoder with the engine's rounding points (vlog_amd/csrc/engine.cpp encode_chunk): the im2col'd
+        mel, the conv1 output, every LayerNorm output, q/k/v, the attention output and the GELU(fc1) output are
+        stored as bf16; the residual stream and every accumulation stay float32."""
+        w = self.w
+        q_ = to_bf16
+        x = q_(np.asarray(mel, dtype=np.float32))
+        x = q_(gelu(conv1d(x, w["model.encoder.conv1.weight"], w["model.encoder.conv1.bias"], 1)))
+        x = gelu(conv1d(x, w["model.encoder.conv2.weight"], w["model.encoder.conv2.bias"], 2))
+        x = (x.transpose(0, 2, 1) + w["model.encoder.embed_positions.weight"][: x.shape[2]]).astype(np.float32)
+        for i in range(self.dims.n_enc_layer):
+            p = f"model.encoder.layers.{i}."
+            h = q_(layer_norm(x, w[p + "self_attn_layer_norm.weight"], w[p + "self_attn_layer_norm.bias"]))
+            q = self._split(q_(self._lin(h, p + "self_attn.q_proj")))
+            k = self._split(q_(self._lin(h, p + "self_attn.k_proj", bias=False)))
+            v = self._split(q_(self._lin(h, p + "self_attn.v_proj")))
+            o = self._attn_enc_bf16(q, k, v)
+            x = x + self._lin(self._merge(o), p + "self_attn.out_proj")
+            h = q_(layer_norm(x, w[p + "final_layer_norm.weight"], w[p + "final_layer_norm.bias"]))
+            x = x + self._lin(q_(gelu(self._lin(h, p + "fc1"))), p + "fc2")
+        return q_(layer_norm(x, w["model.encoder.layer_norm.weight"], w["model.encoder.layer_norm.bias"]))
 
     # ---------------------------------------------------------------- decoder
     def cross_kv(self, enc: np.ndarray) -> List[Tuple[np.ndarray, np.ndarray]]:
@@ -163,7 +199,8 @@ class OracleWhisper:
             h = self._q(layer_norm(x, w[p + "encoder_attn_layer_norm.weight"], w[p + "encoder_attn_layer_norm.bias"]))
             q = self._split(self._q(self._lin(h, p + "encoder_attn.q_proj")))
             ck, cv = cross[i]
-            if ck.shape[0] != B:        # hypotheses sharing one window's cross-KV (beam search)
+            if ck.shape[0] not in (1, B):   # hypotheses sharing one window's cross-KV (beam search);
+                # a single window broadcasts through the batched matmuls without a copy
                 rep = B // ck.shape[0]
                 ck, cv = np.repeat(ck, rep, axis=0), np.repeat(cv, rep, axis=0)
             o, pw = self._attn(q, ck, cv, return_weights=return_cross_attn)

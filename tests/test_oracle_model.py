@@ -35,3 +35,27 @@ def test_encoder_and_decoder_match_transformers():
     a, cache = orc.decode(toks[:, :3], cross)
     b, _ = orc.decode(toks[:, 3:], cross, cache, offset=3)        # KV-cached continuation
     assert np.abs(np.concatenate([a, b], 1) - lg_hf).max() < 1e-4
+
+
+def test_bf16_format_modes_stay_within_rounding_noise():
+    """The engine-numeric-format modes (bf16_enc encoder, bf16_acts decoder) differ from the float32 restatement
+    only by bf16 rounding; the teacher-forced parity helper finds an oracle-generated sequence identical to
+    itself (tests/parity_util.py)."""
+    from oracle.decode import GenerateOptions, generate_one
+    from tests.parity_util import teacher_force
+    from vlog_amd.weights import round_bf16
+    dims = custom_dims("t", 80, 128, 2, 2, 2, 51865, True)
+    sd = round_bf16(synthetic_state_dict(dims, 2, eot_after=20))
+    mel = np.random.default_rng(1).standard_normal((1, 80, 3000)).astype(np.float32)
+    f32 = OracleWhisper(sd, dims, np.float32)
+    bf = OracleWhisper(sd, dims, np.float32, bf16_acts=True, bf16_enc=True)
+    e32, ebf = f32.encode(mel), bf.encode(mel)
+    rms = float(np.sqrt(np.mean(e32 ** 2)))
+    assert np.abs(e32 - ebf).max() < 0.05 * rms and np.abs(e32 - ebf).mean() < 0.01 * rms
+    st = dims.specials
+    prompt = [st.sot, st.lang_token("en"), st.transcribe]
+    opt = GenerateOptions(suppress_tokens=[st.transcribe, st.translate, st.sot, st.sot_prev, st.sot_lm], max_length=60)
+    cross = bf.cross_kv(ebf)
+    r = generate_one(bf, cross, prompt, st, opt)
+    chosen, best, score, ns = teacher_force(bf, cross, prompt, r.tokens, st, opt, len(prompt) + len(r.tokens) < 60)
+    assert np.all(chosen - best >= -1e-9) and abs(score - r.score) < 1e-6 and abs(ns - r.no_speech_prob) < 1e-9
