@@ -149,17 +149,22 @@ int main(int argc, char** argv) {
       });
       std::printf("%s N=%5d K=%5d  launch_gemm        %7.2f us  %7.1f GB/s(W)\n", s.name, s.N, s.K, us, wbytes / us / 1e3);
     }
-    for (int kr : {0, 640, 1280, 2560, 5120}) {
-      if (kr > s.K || (kr > 0 && kr != s.K && s.K <= 1280)) continue;
-      CK(hipMemsetAsync(dC, 0, cbytes, st));
-      if (!launch_dec_ring(a, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st)) { std::printf("ring kr=%d unsupported\n", kr); continue; }
-      CK(hipStreamSynchronize(st));
-      const double err = f32 ? 0.0 : maxdiff();
-      const double us = timeit([&](int r) {
-        launch_dec_ring(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st);
-      });
-      std::printf("%s N=%5d K=%5d  RING kr=%4d        %7.2f us  %7.1f GB/s(W)  rel diff %.1e\n", s.name, s.N, s.K, kr, us,
-                  wbytes / us / 1e3, err);
+    for (int rpb : {0, 32, 64, 96}) {
+      for (int kr : {0, 640, 1280, 2560, 5120}) {
+        if (kr > s.K || (kr > 0 && kr != s.K && s.K <= 1280)) continue;
+        CK(hipMemsetAsync(dC, 0, cbytes, st));
+        if (!launch_dec_ring(a, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb)) {
+          std::printf("ring kr=%d rows=%d unsupported\n", kr, rpb);
+          continue;
+        }
+        CK(hipStreamSynchronize(st));
+        const double err = f32 ? 0.0 : maxdiff();
+        const double us = timeit([&](int r) {
+          launch_dec_ring(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb);
+        });
+        std::printf("%s N=%5d K=%5d  RING kr=%4d rows=%3d %7.2f us  %7.1f GB/s(W)  rel diff %.1e\n", s.name, s.N, s.K, kr,
+                    rpb, us, wbytes / us / 1e3, err);
+      }
     }
     for (int kr : krs) {
       if (kr > s.K) continue;

@@ -137,6 +137,9 @@ struct wm_engine {
   DevBuf gemm_ws, gemm_ws2;  // split-K partial slabs (per decoder slice stream)
   // two-slice decode (decoder_pass): second stream + fork/phase/join events
   bool dec_ring = true;      // ring-pipelined decoder GEMMs for the wide K <= 1280 projections (gemm_dec.hip)
+  int dec_rows = 0;          // > 0: EVERY decoder projection takes the ring GEMM with the rows split into groups of
+                             // this many (one block per 32-column tile x row group x K split); 0: legacy routing
+  int dec_rows_wide = 0;     // row-group size for the wide projections (QKV, fc1; 0 = dec_rows)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
@@ -470,9 +473,18 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   const size_t wsb = 64ull << 20;
   sl.ws->ensure(wsb);
   float* ws = sl.ws->as<float>();
+  // row-group ring routing (dec_rows > 0): decided on the whole pass's rows so slicing never changes a row's
+  // arithmetic; K > 1280 (fc2) splits K into 1280-deep ranges whose slabs the residual+LayerNorm reduce sums
+  auto ring_rows = [&](int N, int K) -> int {
+    if (e->dec_rows <= 0 || sl.total_rows > 1024) return 0;    // long prefills keep the large-tile GEMMs
+    return (N >= 3 * K && e->dec_rows_wide > 0) ? e->dec_rows_wide : e->dec_rows;
+  };
   auto gemm = [&](const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
     const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : 2;
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
+    if (const int rr = ring_rows(N, K)) {
+      if (launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, K <= 1280 ? K : 1280, st, rr)) return;
+    }
     // Wide projections with K <= 1280 (self-attention QKV, fc1: N >= 3K) take the ring-pipelined GEMM: one
     // pass over K, epilogue applied in place, no split-K slabs and no combine launch.  The square ones (out,
     // cq, cout) and fc2 (K = 4d) keep the split-K skinny path, which measured faster for them in the decode
@@ -507,7 +519,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   CrossFuse fz;
   {
     GemmEpi ep = epi_of(EPI_BF16, q, d, W.cq_b);
-    const int sk = skinny_splits(rows, d, d, wsb);
+    const int sk = ring_rows(d, d) ? 1 : skinny_splits(rows, d, d, wsb);
     if ((e->cross_fuse & 1) && !(attn && align_map) && sk > 1) {
       ep.defer_combine = 1;
       fz.q_part = ws; fz.q_splits = sk; fz.q_rows = rows; fz.q_bias = W.cq_b;
@@ -1007,6 +1019,8 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     e->device = device;
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_ROWS")) e->dec_rows = std::max(0, std::min(160, std::atoi(v)));
+    if (const char* v = std::getenv("VLOG_AMD_DEC_ROWS_WIDE")) e->dec_rows_wide = std::max(0, std::min(160, std::atoi(v)));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));
@@ -1187,6 +1201,8 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     const std::string k(key);
     if (k == "decode_split") e->dec_split = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
+    else if (k == "decode_ring_rows") e->dec_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 160));
+    else if (k == "decode_ring_rows_wide") e->dec_rows_wide = (int)std::max<int64_t>(0, std::min<int64_t>(value, 160));
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));

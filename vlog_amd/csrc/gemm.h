@@ -64,5 +64,7 @@ bool launch_dec_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N,
                      size_t ws_bytes, int KR, hipStream_t st);
 void launch_splitk_combine(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st);
 // Ring-pipelined decoder-row path (gemm_dec.hip): M <= 160; kr = K range per block (0 = whole K up to 1280).
+// rows_per_block > 0: the rows are split into groups of that many (32..160) — one block per (32-column tile, row
+// group, K split); the row groups of a tile share its weight panel through one XCD's L2 (any M).
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     size_t ws_bytes, int kr, hipStream_t st);
+                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block = 0);

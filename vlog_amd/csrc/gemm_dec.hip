@@ -11,6 +11,7 @@
 // summation order is a function of (N, K, KR) only.
 #include "gemm.h"
 #include "gemm_epi.h"
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -182,15 +183,17 @@ __device__ __forceinline__ void vm_wait(int n) {
 template <int MF, int KIND, int R>
 __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
                                                        int K, GemmEpi epi, int tiles_n, int splitk, int kr,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, int rgroups) {
   static_assert(MF % 2 == 0, "MF must be even");
   constexpr int ROWS = MF * 16, HALF = MF / 2, SLOT = (ROWS + 32) * 64, DA = ROWS / 32, DPP = DA + 1;
   __shared__ __attribute__((aligned(16))) bf16 smem[R * SLOT];
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int split = wgid % splitk, tile = wgid / splitk;
-  const int n0 = tile * 32;
+  // consecutive ids (one XCD) = the K splits and row groups of one 32-column tile: its weight panel is read from
+  // HBM once and served to the other row groups from that XCD's L2
+  const int split = wgid % splitk, rg = (wgid / splitk) % rgroups, tile = wgid / (splitk * rgroups);
+  const int n0 = tile * 32, m0 = rg * ROWS;
   const int kb = split * kr, klen = min(kr, K - kb), NP = klen / 64;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid & 1, wr = wid >> 1;
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   for (int j = 0; j < DA; ++j) {
     const int row = wid * (ROWS / 4) + j * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    const int gr = min(row, M - 1);
+    const int gr = min(m0 + row, M - 1);
     const long long off = a.rpb ? (long long)(gr / a.rpb) * a.bstride + (long long)(gr % a.rpb) * a.ld : (long long)gr * a.ld;
     srcA[j] = a.ptr + off + kb + ch * 8;
   }
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   if (col0 >= N) return;
 #pragma unroll
   for (int i = 0; i < HALF; ++i) {
-    const int row = (wr * HALF + i) * 16 + (lane & 15);
+    const int row = m0 + (wr * HALF + i) * 16 + (lane & 15);
     if (row >= M) continue;
     if (to_slab)
       *(f32x4*)(part + ((long long)split * M + row) * N + col0) = acc[i];
@@ -264,26 +267,30 @@ static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
                      int splitk, int kr, hipStream_t st) {
   constexpr int R = MF <= 4 ? 8 : MF <= 8 ? 7 : 6;     // (MF*16 + 32) * 128 B per slot, <= 144 KiB in all
   const int tiles_n = (N + 31) / 32;
-  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R>), dim3(tiles_n * splitk), dim3(256), 0, st, a, w, ldw, M, N, K, epi,
-                     tiles_n, splitk, kr, ws);
+  const int rgroups = (M + MF * 16 - 1) / (MF * 16);
+  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R>), dim3(tiles_n * rgroups * splitk), dim3(256), 0, st, a, w, ldw, M, N,
+                     K, epi, tiles_n, splitk, kr, ws, rgroups);
   WM_LAUNCH_CHECK("dec_ring_kernel");
 }
 
+// rows_per_block 0: one row group covering every row (MF from M); else 32 / 64 / 96 / 128 / 160 rows per block
+// and ceil(M / rows) row groups.
 template <int KIND>
 static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
-                          float* ws, int splitk, int kr, hipStream_t st) {
-  if (M <= 32) run_ring<2, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (M <= 64) run_ring<4, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (M <= 96) run_ring<6, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (M <= 128) run_ring<8, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+                          float* ws, int splitk, int kr, int rows_per_block, hipStream_t st) {
+  const int rows = rows_per_block > 0 ? std::min(rows_per_block, ((M + 31) / 32) * 32) : M;
+  if (rows <= 32) run_ring<2, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (rows <= 64) run_ring<4, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (rows <= 96) run_ring<6, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (rows <= 128) run_ring<8, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
   else run_ring<10, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
-// Ring path: M <= 160, N % 4 == 0, K % 64 == 0.  kr = K range per block (0: the whole K up to 1280, else split
-// into ceil(K / 1280) ranges).  Returns false when unsupported.
+// Ring path: N % 4 == 0, K % 64 == 0; M <= 160 for one row group, any M with rows_per_block > 0.  kr = K range
+// per block (0: the whole K up to 1280, else split into ceil(K / 1280) ranges).  Returns false when unsupported.
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     size_t ws_bytes, int kr, hipStream_t st) {
-  if (M > 160 || N % 4 != 0 || K % 64 != 0) return false;
+                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block) {
+  if ((rows_per_block <= 0 && M > 160) || rows_per_block > 160 || N % 4 != 0 || K % 64 != 0) return false;
   if (kr <= 0) kr = K <= 1280 ? K : ((K + (K + 1279) / 1280 - 1) / ((K + 1279) / 1280) + 63) / 64 * 64;
   if (kr % 64 != 0) return false;
   const int splitk = (K + kr - 1) / kr;
@@ -292,14 +299,14 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   switch (epi.kind) {
-    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
-    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
-    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
-    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
-    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
+    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
+    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
+    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
+    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
     default: return false;
   }
-  if (slab) launch_splitk_combine(ws, splitk, M, N, epi, st);
+  if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
   return true;
 }
 
