@@ -38,8 +38,9 @@ def log_softmax(x: np.ndarray) -> np.ndarray:
 
 def apply_rules(logits: np.ndarray, sampled: Sequence[int], st, suppress_tokens: Sequence[int],
                 suppress_blank: bool, max_initial_timestamp_index: Optional[int],
-                with_timestamps: bool = True) -> np.ndarray:
-    """logits [V] for ONE hypothesis; `sampled` = tokens generated after the prompt."""
+                with_timestamps: bool = True, force_timestamps: bool = True) -> np.ndarray:
+    """logits [V] for ONE hypothesis; `sampled` = tokens generated after the prompt.  force_timestamps=False
+    stops before the last rule (diagnostics: the logits the forcing decision is taken on)."""
     x = np.array(logits, dtype=np.float64, copy=True)
     first = len(sampled) == 0
     if suppress_blank and first:
@@ -66,6 +67,8 @@ def apply_rules(logits: np.ndarray, sampled: Sequence[int], st, suppress_tokens:
         x[:tb] = NEG_INF
         if max_initial_timestamp_index is not None:
             x[tb + max_initial_timestamp_index + 1:] = NEG_INF
+    if not force_timestamps:
+        return x
     lp = log_softmax(x)
     ts_lp = np.logaddexp.reduce(lp[tb:])
     if ts_lp > np.max(lp[:tb]):

@@ -166,6 +166,17 @@ int main(int argc, char** argv) {
                     rpb, us, wbytes / us / 1e3, err);
       }
     }
+    for (int nc : {2, 4}) {
+      CK(hipMemsetAsync(dC, 0, cbytes, st));
+      if (!launch_dec_oneshot(a, dW, s.K, M, s.N, s.K, ep, ws, wsb, nc, st)) { std::printf("oneshot nc=%d unsupported\n", nc); continue; }
+      CK(hipStreamSynchronize(st));
+      const double err = f32 ? 0.0 : maxdiff();
+      const double us = timeit([&](int r) {
+        launch_dec_oneshot(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, nc, st);
+      });
+      std::printf("%s N=%5d K=%5d  ONESHOT nc=%d        %7.2f us  %7.1f GB/s(W)  rel diff %.1e\n", s.name, s.N, s.K, nc, us,
+                  wbytes / us / 1e3, err);
+    }
     for (int kr : krs) {
       if (kr > s.K) continue;
       CK(hipMemsetAsync(dC, 0, cbytes, st));

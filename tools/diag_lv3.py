@@ -42,8 +42,9 @@ variants = [
     ("fuse_off", {"cross_attn_fuse": 0}),
     ("projected", {"cross_mode": 0}),
     ("rows32", {"decode_ring_rows": 32}),
+    ("oneshot", {"decode_gemm": 1}),
 ]
-base = {"decode_ring_gemm": 1, "cross_attn_fuse": 1, "cross_mode": 1, "decode_ring_rows": 0}
+base = {"decode_ring_gemm": 1, "cross_attn_fuse": 1, "cross_mode": 1, "decode_ring_rows": 0, "decode_gemm": 0}
 toks = {}
 for name, kv in variants:
     for k, v in base.items():
@@ -60,4 +61,5 @@ for name, kv in variants:
     rows = [window_parity(orc, encw[w], prompt, res[w], dims.specials, opt, w) for w in check]
     same = {v: sum(a == b for a, b in zip(toks[name], toks[v])) for v in toks}
     print(json.dumps({"variant": name, "s": round(dt, 3), "margins": {r.window: round(r.min_margin, 4) for r in rows},
+                      "tie_margins": {r.window: [round(r.min_margin_rule_tie, 4), r.worst_step, round(r.worst_gap, 4)] for r in rows},
                       "identical": {r.window: r.identical for r in rows}, "same_tokens_as": same}), flush=True)

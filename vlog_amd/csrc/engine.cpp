@@ -140,6 +140,8 @@ struct wm_engine {
   int dec_rows = 0;          // > 0: EVERY decoder projection takes the ring GEMM with the rows split into groups of
                              // this many (one block per 32-column tile x row group x K split); 0: legacy routing
   int dec_rows_wide = 0;     // row-group size for the wide projections (QKV, fc1; 0 = dec_rows)
+  int dec_gemm = 0;          // 1: every decoder projection of a pass with <= 1024 rows takes the one-shot GEMM
+                             // (gemm_dec.hip launch_dec_oneshot); 0: the ring / skinny routing below
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
@@ -482,6 +484,9 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   auto gemm = [&](const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
     const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : 2;
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
+    if (e->dec_gemm == 1 && sl.total_rows <= 1024) {
+      if (launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
+    }
     if (const int rr = ring_rows(N, K)) {
       if (launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, K <= 1280 ? K : 1280, st, rr)) return;
     }
@@ -519,7 +524,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   CrossFuse fz;
   {
     GemmEpi ep = epi_of(EPI_BF16, q, d, W.cq_b);
-    const int sk = ring_rows(d, d) ? 1 : skinny_splits(rows, d, d, wsb);
+    const int sk = (ring_rows(d, d) || (e->dec_gemm == 1 && sl.total_rows <= 1024)) ? 1 : skinny_splits(rows, d, d, wsb);
     if ((e->cross_fuse & 1) && !(attn && align_map) && sk > 1) {
       ep.defer_combine = 1;
       fz.q_part = ws; fz.q_splits = sk; fz.q_rows = rows; fz.q_bias = W.cq_b;
@@ -1020,6 +1025,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_ROWS")) e->dec_rows = std::max(0, std::min(160, std::atoi(v)));
+    if (const char* v = std::getenv("VLOG_AMD_DEC_GEMM")) e->dec_gemm = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_ROWS_WIDE")) e->dec_rows_wide = std::max(0, std::min(160, std::atoi(v)));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
@@ -1201,6 +1207,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     const std::string k(key);
     if (k == "decode_split") e->dec_split = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
+    else if (k == "decode_gemm") e->dec_gemm = value != 0;
     else if (k == "decode_ring_rows") e->dec_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 160));
     else if (k == "decode_ring_rows_wide") e->dec_rows_wide = (int)std::max<int64_t>(0, std::min<int64_t>(value, 160));
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);

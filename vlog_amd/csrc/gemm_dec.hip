@@ -333,3 +333,126 @@ void launch_dec_gemm_body(const GemmA& a, const bf16* w, long long ldw, int M, i
 #undef DG_CASE
   throw std::runtime_error("launch_dec_gemm_body: unsupported KR/abl");
 }
+
+// ------------------------------------------------------------------------------------------------------
+// One-shot decoder GEMM (the default decoder projection path): one 512-thread block = 32 rows x NC*16 output
+// columns x a K range of <= 1280.  The K range is split over the 8 waves (up to 5 k-steps of 32 each); every
+// wave issues ALL its loads at once — its W fragments (the HBM stream) and its A fragments (L2-resident
+// activations), 16 B per lane straight into MFMA operand registers, no LDS staging — so a block pays one
+// memory round trip, with up to 160 KB in flight per block.  The 8 per-wave partial tiles are summed through
+// LDS in wave order (deterministic), then the epilogue is applied in place (or a split-K slab is written when
+// K > 1280).  Row groups of one column tile get consecutive ids (one XCD): the weight panel is fetched from HBM
+// once and served to the other row groups by that XCD's L2.  Replaces, at decoder row counts, split-K slabs
+// whose write + re-read cost more than the weight stream itself (tools/dec_gemm_bench: slab stores were ~half
+// of the skinny kernel's time at M = 150).
+template <int NC, int KIND>
+__global__ __launch_bounds__(512) void dec_oneshot_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M,
+                                                          int N, int K, GemmEpi epi, int rgroups, int splitk, int kr,
+                                                          float* __restrict__ part) {
+  constexpr int KSMAX = 5;
+  __shared__ __attribute__((aligned(16))) f32x4 sred[8][2 * NC][64];
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int split = wgid % splitk, rg = (wgid / splitk) % rgroups, tile = wgid / (splitk * rgroups);
+  const int n0 = tile * (NC * 16), m0 = rg * 32;
+  const int kb = split * kr, klen = min(kr, K - kb);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nks = klen / 32;                                    // k-steps of this block
+  const int s0 = wv * nks / 8, s1 = (wv + 1) * nks / 8;         // this wave's k-steps [s0, s1)
+  const int kl = kb + 8 * (lane >> 4);
+  bf16x8 fw[KSMAX][NC], fa[KSMAX][2];
+#pragma unroll
+  for (int s = 0; s < KSMAX; ++s) {
+    if (s0 + s < s1) {
+      const int k = kl + 32 * (s0 + s);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int n = min(n0 + c * 16 + (lane & 15), N - 1);
+        fw[s][c] = *(const bf16x8*)(w + (long long)n * ldw + k);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = min(m0 + i * 16 + (lane & 15), M - 1);
+        const long long off = a.rpb ? (long long)(m / a.rpb) * a.bstride + (long long)(m % a.rpb) * a.ld : (long long)m * a.ld;
+        fa[s][i] = *(const bf16x8*)(a.ptr + off + k);
+      }
+    }
+  }
+  f32x4 acc[NC][2];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[c][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KSMAX; ++s) {
+    if (s0 + s < s1) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[s][c], fa[s][i], acc[c][i], 0, 0, 0);
+    }
+  }
+  // W fragment as the MFMA A operand: acc[c][i] holds C^T, lane l has row m0 + 16 i + (l & 15) and the 4
+  // consecutive columns n0 + 16 c + 4 (l >> 4) + e
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) sred[wv][c * 2 + i][lane] = acc[c][i];
+  __syncthreads();
+  const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
+  for (int idx = tid; idx < 2 * NC * 64; idx += 512) {
+    const int f = idx >> 6, ln = idx & 63;
+    f32x4 v = sred[0][f][ln];
+#pragma unroll
+    for (int w2 = 1; w2 < 8; ++w2) v += sred[w2][f][ln];
+    const int c = f >> 1, i = f & 1;
+    const int row = m0 + i * 16 + (ln & 15), col0 = n0 + c * 16 + 4 * (ln >> 4);
+    if (row >= M || col0 >= N) continue;
+    if (to_slab)
+      *(f32x4*)(part + ((long long)split * M + row) * N + col0) = v;
+    else
+      apply_epi4<KIND>(epi, row, col0, v);
+  }
+}
+
+template <int NC, int KIND>
+static void run_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                        int splitk, int kr, hipStream_t st) {
+  const int tiles_n = (N + NC * 16 - 1) / (NC * 16), rgroups = (M + 31) / 32;
+  hipLaunchKernelGGL((dec_oneshot_kernel<NC, KIND>), dim3(tiles_n * rgroups * splitk), dim3(512), 0, st, a, w, ldw, M, N,
+                     K, epi, rgroups, splitk, kr, ws);
+  WM_LAUNCH_CHECK("dec_oneshot_kernel");
+}
+
+template <int KIND>
+static void dispatch_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
+                             float* ws, int splitk, int kr, int nc, hipStream_t st) {
+  if (nc == 4) run_oneshot<4, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_oneshot<2, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+}
+
+// One-shot path: K % 32 == 0, N % 4 == 0, any M (rows in groups of 32).  K ranges of at most 1280 (8 waves x 5
+// k-steps): K <= 1280 in one range, else split into equal ranges (multiples of 32) with slabs combined by
+// launch_splitk_combine.  nc = 16-column fragments per block (2 or 4).  Returns false when unsupported.
+bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                        size_t ws_bytes, int nc, hipStream_t st) {
+  if (M <= 0 || N % 4 != 0 || K % 32 != 0 || (nc != 2 && nc != 4)) return false;
+  const int ks = K / 32;
+  const int splitk = (ks + 39) / 40;                       // ranges of <= 40 k-steps (1280)
+  if (ks % splitk != 0) return false;
+  const int kr = K / splitk;
+  const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
+  if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
+  if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
+  switch (epi.kind) {
+    case EPI_BF16: dispatch_oneshot<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, nc, st); break;
+    case EPI_RESID_F32: dispatch_oneshot<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, nc, st); break;
+    case EPI_F32: dispatch_oneshot<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, nc, st); break;
+    case EPI_DEC_QKV: dispatch_oneshot<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, nc, st); break;
+    case EPI_RESID_LN: dispatch_oneshot<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, nc, st); break;
+    default: return false;
+  }
+  if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
+  return true;
+}
