@@ -150,9 +150,13 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   slice's weight GEMMs overlapping the other's cross-attention.  Results are bit-identical
  *   either way; off by default because the overlap measured slower on MI355X (the GEMM blocks queue behind
  *   the cross-attention blocks).
- *   "decode_ring_gemm" (default 1): the wide decoder projections with K <= 1280 (self-attention QKV, fc1)
- *   use the ring-pipelined GEMM (one pass over K, no split-K slabs or combine launch); 0 uses the split-K
- *   skinny GEMM for every decoder projection.
+ *   "decode_ring_gemm" (default 1): 0 disables the all-rows ring GEMM (plan value 0 below falls back to the
+ *   split-K skinny GEMM).
+ *   "decode_gemm_plan" (default 1): preset routing of the six decoder projections (qkv, out, cq, cout, fc1, fc2)
+ *   for passes of <= 1024 rows; 0 = round-1 routing (ring for qkv/fc1, skinny split-K for the rest), 1 = the
+ *   per-projection fastest at 150 rows (tools/dec_gemm_bench).  "decode_gemm.<proj>" sets one projection:
+ *   > 0 ring GEMM with the rows in groups of that many, 0 all-rows ring, -1 skinny split-K, -2 one-shot GEMM.
+ *   Routes differ in K summation order (results agree to f32 rounding, not bit for bit).
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its
  *   (window, head, key split) items with a grid stride; 0 launches one block per item.
  *   "cross_attn_fuse" (default 1): bit 0 folds the cq projection's split-K combine into the cross-attention

@@ -41,10 +41,9 @@ variants = [
     ("ring_off", {"decode_ring_gemm": 0}),
     ("fuse_off", {"cross_attn_fuse": 0}),
     ("projected", {"cross_mode": 0}),
-    ("rows32", {"decode_ring_rows": 32}),
-    ("oneshot", {"decode_gemm": 1}),
+    ("plan0", {"decode_gemm_plan": 0}),
 ]
-base = {"decode_ring_gemm": 1, "cross_attn_fuse": 1, "cross_mode": 1, "decode_ring_rows": 0, "decode_gemm": 0}
+base = {"decode_ring_gemm": 1, "cross_attn_fuse": 1, "cross_mode": 1, "decode_gemm_plan": 1}
 toks = {}
 for name, kv in variants:
     for k, v in base.items():

@@ -99,6 +99,11 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+// Decoder projections (index of wm_engine::dec_plan)
+enum DecProj { DEC_QKV = 0, DEC_OUT, DEC_CQ, DEC_COUT, DEC_FC1, DEC_FC2, DEC_NPROJ };
+static const char* kDecProjNames[DEC_NPROJ] = {"qkv", "out", "cq", "cout", "fc1", "fc2"};
+static const int kDecPlanPresets[2][DEC_NPROJ] = {{0, -1, -1, -1, 0, -1}, {96, 32, 32, 32, 0, -1}};
+
 // Decoder weight pointers per layer (resolved once: the arena layout is fixed at wm_create).
 struct DecLayerW {
   const bf16 *qkv_w, *out_w, *cq_w, *cout_w, *fc1_w, *fc2_w;
@@ -137,11 +142,14 @@ struct wm_engine {
   DevBuf gemm_ws, gemm_ws2;  // split-K partial slabs (per decoder slice stream)
   // two-slice decode (decoder_pass): second stream + fork/phase/join events
   bool dec_ring = true;      // ring-pipelined decoder GEMMs for the wide K <= 1280 projections (gemm_dec.hip)
-  int dec_rows = 0;          // > 0: EVERY decoder projection takes the ring GEMM with the rows split into groups of
-                             // this many (one block per 32-column tile x row group x K split); 0: legacy routing
-  int dec_rows_wide = 0;     // row-group size for the wide projections (QKV, fc1; 0 = dec_rows)
-  int dec_gemm = 0;          // 1: every decoder projection of a pass with <= 1024 rows takes the one-shot GEMM
-                             // (gemm_dec.hip launch_dec_oneshot); 0: the ring / skinny routing below
+  // Decoder projection plan, per projection (DEC_QKV .. DEC_FC2), for passes of <= 1024 rows:
+  //   > 0  ring GEMM with the rows in groups of that many (one block per 32-column tile x row group x K split)
+  //     0  ring GEMM, all rows in one block (passes of <= 160 rows; wide projections only)
+  //    -1  skinny split-K GEMM (gemm.hip launch_gemm)
+  //    -2  one-shot GEMM (gemm_dec.hip launch_dec_oneshot)
+  // Preset 1 (default) is the fastest per projection measured at 150 rows (tools/dec_gemm_bench);
+  // preset 0 is round 1's routing.
+  int dec_plan[6] = {96, 32, 32, 32, 0, -1};
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
@@ -475,29 +483,19 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   const size_t wsb = 64ull << 20;
   sl.ws->ensure(wsb);
   float* ws = sl.ws->as<float>();
-  // row-group ring routing (dec_rows > 0): decided on the whole pass's rows so slicing never changes a row's
-  // arithmetic; K > 1280 (fc2) splits K into 1280-deep ranges whose slabs the residual+LayerNorm reduce sums
-  auto ring_rows = [&](int N, int K) -> int {
-    if (e->dec_rows <= 0 || sl.total_rows > 1024) return 0;    // long prefills keep the large-tile GEMMs
-    return (N >= 3 * K && e->dec_rows_wide > 0) ? e->dec_rows_wide : e->dec_rows;
-  };
-  auto gemm = [&](const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
+  // The route of each projection follows the whole pass's rows (sl.total_rows), so slicing a pass never changes
+  // a row's arithmetic.  Long prefills (> 1024 rows) keep the large-tile GEMMs.
+  auto plan_of = [&](int proj) -> int { return sl.total_rows > 1024 ? -1 : e->dec_plan[proj]; };
+  auto gemm = [&](int proj, const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
     const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : 2;
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
-    if (e->dec_gemm == 1 && sl.total_rows <= 1024) {
-      if (launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
-    }
-    if (const int rr = ring_rows(N, K)) {
-      if (launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, K <= 1280 ? K : 1280, st, rr)) return;
-    }
-    // Wide projections with K <= 1280 (self-attention QKV, fc1: N >= 3K) take the ring-pipelined GEMM: one
-    // pass over K, epilogue applied in place, no split-K slabs and no combine launch.  The square ones (out,
-    // cq, cout) and fc2 (K = 4d) keep the split-K skinny path, which measured faster for them in the decode
-    // step.  The choice follows the whole pass's rows (sl.total_rows) so slicing never changes a row's
-    // arithmetic.
-    if (!(e->dec_ring && K <= 1280 && N >= 3 * K && sl.total_rows <= 160 &&
-          launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st)))
-      launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
+    const int p = plan_of(proj);
+    if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
+    // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
+    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, K <= 1280 ? K : 1280, st, p)) return;
+    if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
+      return;
+    launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
   };
   // residual-producing GEMMs also apply the LayerNorm that consumes the residual (EPI_RESID_LN: fused into
   // the split-K combine on the skinny path): out -> ln2, cout -> ln3, fc2 -> next layer's ln1
@@ -512,24 +510,24 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, W.qkv_b);
     ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
     ep.d = d; ep.n_head = H; ep.head_dim = 64; ep.n_ctx = C;
-    gemm(amat(hb, d), W.qkv_w, d, 3 * d, d, ep);
+    gemm(DEC_QKV, amat(hb, d), W.qkv_w, d, 3 * d, d, ep);
   }
   {
     ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
     launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
   }
-  gemm(amat(ao, d), W.out_w, d, d, d, resid_ln(W.ln2_w, W.ln2_b, W.out_b));
+  gemm(DEC_OUT, amat(ao, d), W.out_w, d, d, d, resid_ln(W.ln2_w, W.ln2_b, W.out_b));
   // cq: when the skinny split-K path runs it and no attention is captured, its slabs stay in the scratch and
   // the cross-attention kernel sums them while loading q (no combine launch)
   CrossFuse fz;
   {
     GemmEpi ep = epi_of(EPI_BF16, q, d, W.cq_b);
-    const int sk = (ring_rows(d, d) || (e->dec_gemm == 1 && sl.total_rows <= 1024)) ? 1 : skinny_splits(rows, d, d, wsb);
+    const int sk = plan_of(DEC_CQ) != -1 ? 1 : skinny_splits(rows, d, d, wsb);
     if ((e->cross_fuse & 1) && !(attn && align_map) && sk > 1) {
       ep.defer_combine = 1;
       fz.q_part = ws; fz.q_splits = sk; fz.q_rows = rows; fz.q_bias = W.cq_b;
     }
-    gemm(amat(hb, d), W.cq_w, d, d, d, ep);
+    gemm(DEC_CQ, amat(hb, d), W.cq_w, d, d, d, ep);
   }
   if ((e->cross_fuse & 2) && e->cross_mode == 0) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   float* probs = nullptr;
@@ -578,17 +576,17 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
                       e->cross_cap, fz, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
   }
   if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
-  gemm(amat(ao, d), W.cout_w, d, d, d, resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
+  gemm(DEC_COUT, amat(ao, d), W.cout_w, d, d, d, resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
   {
     GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, W.fc1_b);
     ep.act = 1;
-    gemm(amat(hb, d), W.fc1_w, d, 4 * d, d, ep);
+    gemm(DEC_FC1, amat(hb, d), W.fc1_w, d, 4 * d, d, ep);
   }
   if (l + 1 < L) {
     const auto& Wn = dec_weights(e)[l + 1];
-    gemm(amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, resid_ln(Wn.ln1_w, Wn.ln1_b, W.fc2_b));
+    gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, resid_ln(Wn.ln1_w, Wn.ln1_b, W.fc2_b));
   } else {
-    gemm(amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, epi_of(EPI_RESID_F32, x, d, W.fc2_b));
+    gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, epi_of(EPI_RESID_F32, x, d, W.fc2_b));
   }
 }
 
@@ -1024,9 +1022,10 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     e->device = device;
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
-    if (const char* v = std::getenv("VLOG_AMD_DEC_ROWS")) e->dec_rows = std::max(0, std::min(160, std::atoi(v)));
-    if (const char* v = std::getenv("VLOG_AMD_DEC_GEMM")) e->dec_gemm = std::atoi(v) != 0;
-    if (const char* v = std::getenv("VLOG_AMD_DEC_ROWS_WIDE")) e->dec_rows_wide = std::max(0, std::min(160, std::atoi(v)));
+    if (const char* v = std::getenv("VLOG_AMD_DEC_PLAN")) {
+      const int p = std::atoi(v) != 0;
+      for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[p][i];
+    }
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));
@@ -1207,9 +1206,17 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     const std::string k(key);
     if (k == "decode_split") e->dec_split = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
-    else if (k == "decode_gemm") e->dec_gemm = value != 0;
-    else if (k == "decode_ring_rows") e->dec_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 160));
-    else if (k == "decode_ring_rows_wide") e->dec_rows_wide = (int)std::max<int64_t>(0, std::min<int64_t>(value, 160));
+    else if (k == "decode_gemm_plan") {
+      if (value != 0 && value != 1) throw std::runtime_error("wm_set_option: decode_gemm_plan is 0 or 1");
+      for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[value][i];
+    } else if (k.rfind("decode_gemm.", 0) == 0) {
+      const std::string pj = k.substr(12);
+      int i = 0;
+      while (i < DEC_NPROJ && pj != kDecProjNames[i]) ++i;
+      if (i == DEC_NPROJ) throw std::runtime_error("wm_set_option: unknown projection " + pj);
+      if (value < -2 || value > 160) throw std::runtime_error("wm_set_option: decode_gemm.<proj> in [-2, 160]");
+      e->dec_plan[i] = (int)value;
+    }
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
