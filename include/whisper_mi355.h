@@ -123,6 +123,16 @@ int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_
 int wm_align(wm_engine* e, int32_t slot, int32_t sot_len, const int32_t* h_sot, int32_t n_text, const int32_t* h_text,
              int32_t num_frames, const int32_t* h_heads, int32_t n_heads, int32_t median_filter_width, float* h_probs,
              int32_t* h_text_idx, int32_t* h_time_idx, int32_t* h_path_len, void* stream);
+/* wm_align over a batch of windows (faster-whisper add_word_timestamps over a batch of segments, as the
+ * batched pipeline runs it; one teacher-forced decoder pass per chunk of windows and one batched DTW launch
+ * instead of one wm_align per window).  Item i: window slot h_slots[i], text tokens
+ * h_text[h_text_off[i] .. h_text_off[i+1]), h_num_frames[i] mel frames.  Outputs: probabilities at
+ * h_probs[h_text_off[i] + k]; DTW path of item i at h_text_idx / h_time_idx + h_path_off[i] (capacity
+ * n_text_i + 1 + num_frames_i / 2), length h_path_len[i]. */
+int wm_align_batch(wm_engine* e, int32_t n, const int32_t* h_slots, int32_t sot_len, const int32_t* h_sot,
+                   const int32_t* h_text_off, const int32_t* h_text, const int32_t* h_num_frames, const int32_t* h_heads,
+                   int32_t n_heads, int32_t median_filter_width, float* h_probs, const int64_t* h_path_off,
+                   int32_t* h_text_idx, int32_t* h_time_idx, int32_t* h_path_len, void* stream);
 /* DTW alone on a device cost matrix d_cost[n][m] (openai dtw semantics); path as for wm_align. */
 int wm_dtw(wm_engine* e, const float* d_cost, int32_t n, int32_t m, int32_t* h_text_idx, int32_t* h_time_idx,
            int32_t* h_path_len, void* stream);

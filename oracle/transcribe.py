@@ -48,6 +48,118 @@ def _split(tokens, tb, time_offset, segment_size, segment_duration, seek):
     return out, seek, single
 
 
+# ----------------------------------------------------------------------------------------------- word timestamps
+# faster-whisper 1.1.x `find_alignment` / `add_word_timestamps` and openai `merge_punctuations` [FW↑], restated
+# here independently of vlog_amd/transcribe.py so the product's host logic can be compared against it.
+
+PREPEND = "\"'“¿([{-"
+APPEND = "\"'.。,，!！?？:：”)]}、"
+SENTENCE_END = ".。!！?？"
+
+
+def words_from_alignment(tok, text_tokens, probs, text_idx, time_idx, tokens_per_second=50):
+    """One window's alignment -> [dict(word, tokens, start, end, probability)] (find_alignment's tail)."""
+    words, word_tokens = tok.split_to_word_tokens(list(text_tokens) + [tok.eot])
+    if len(word_tokens) <= 1:
+        return []
+    bounds = [0]
+    for wt in word_tokens[:-1]:
+        bounds.append(bounds[-1] + len(wt))
+    if len(bounds) <= 1:
+        return []
+    text_idx, time_idx = np.asarray(text_idx), np.asarray(time_idx)
+    is_jump = np.concatenate([[True], text_idx[1:] != text_idx[:-1]])
+    jump_t = time_idx[is_jump] / tokens_per_second
+    out = []
+    for k in range(len(bounds) - 1):
+        a, b = bounds[k], bounds[k + 1]
+        out.append(dict(word=words[k], tokens=list(word_tokens[k]), start=jump_t[a], end=jump_t[b],
+                        probability=np.mean(probs[a:b])))
+    return out
+
+
+def merge_punctuations(ws, prepended=PREPEND, appended=APPEND):
+    """openai merge_punctuations on a word list (in place)."""
+    j = len(ws) - 1
+    for i in range(len(ws) - 2, -1, -1):
+        a, b = ws[i], ws[j]
+        if a["word"].startswith(" ") and a["word"].strip() in prepended:
+            b["word"], b["tokens"] = a["word"] + b["word"], a["tokens"] + b["tokens"]
+            a["word"], a["tokens"] = "", []
+        else:
+            j = i
+    i = 0
+    for j in range(1, len(ws)):
+        a, b = ws[i], ws[j]
+        if not a["word"].endswith(" ") and b["word"] in appended:
+            a["word"], a["tokens"] = a["word"] + b["word"], a["tokens"] + b["tokens"]
+            b["word"], b["tokens"] = "", []
+        else:
+            i = j
+
+
+def add_word_timestamps(groups, tok, alignments, last_speech, prepended=PREPEND, appended=APPEND):
+    """groups: per window, its split segments (dicts with seek/start/end/tokens; modified in place: start/end
+    adjusted, `words` added); alignments: per window, words_from_alignment(...) of all its text tokens.
+    -> the new last speech timestamp."""
+    stats = []
+    for al in alignments:
+        d = np.array([w["end"] - w["start"] for w in al])
+        d = d[d.nonzero()]
+        med = min(0.7, float(np.median(d))) if len(d) else 0.0
+        mx = 2 * med
+        if len(d):
+            for i in range(1, len(al)):
+                if al[i]["end"] - al[i]["start"] > mx:
+                    if al[i]["word"] in SENTENCE_END:
+                        al[i]["end"] = al[i]["start"] + mx
+                    elif al[i - 1]["word"] in SENTENCE_END:
+                        al[i]["start"] = al[i]["end"] - mx
+        merge_punctuations(al, prepended, appended)
+        stats.append((med, mx))
+    for g, segs_ in enumerate(groups):
+        al, (med, mx) = alignments[g], stats[g]
+        off = segs_[0]["seek"] / 100.0
+        wi = 0
+        for sub in segs_:
+            need = len([t for t in sub["tokens"] if t < tok.eot])
+            got, words = 0, []
+            while wi < len(al) and got < need:
+                w = al[wi]
+                if w["word"]:
+                    words.append(dict(word=w["word"], start=round(off + w["start"], 2), end=round(off + w["end"], 2),
+                                      probability=w["probability"]))
+                got += len(w["tokens"])
+                wi += 1
+            if words:
+                w0 = words[0]
+                if w0["end"] - last_speech > 4 * med and (
+                        w0["end"] - w0["start"] > mx or (len(words) > 1 and words[1]["end"] - w0["start"] > 2 * mx)):
+                    if len(words) > 1 and words[1]["end"] - words[1]["start"] > mx:
+                        cut = max(words[1]["end"] / 2, words[1]["end"] - mx)
+                        w0["end"] = words[1]["start"] = cut
+                    w0["start"] = max(0, w0["end"] - mx)
+                if sub["start"] < w0["end"] and sub["start"] - 0.5 > w0["start"]:
+                    w0["start"] = max(0, min(w0["end"] - med, sub["start"]))
+                else:
+                    sub["start"] = w0["start"]
+                wl = words[-1]
+                if sub["end"] > wl["start"] and sub["end"] + 0.5 < wl["end"]:
+                    wl["end"] = max(wl["start"] + med, sub["end"])
+                else:
+                    sub["end"] = wl["end"]
+                last_speech = sub["end"]
+            sub["words"] = words
+    return last_speech
+
+
+def last_word_end(segs_):
+    for s in reversed(segs_):
+        for w in reversed(s.get("words") or []):
+            return w["end"]
+    return segs_[-1]["end"] if segs_ else None
+
+
 class OracleBackend:
     """The oracle's own encoder + decoder for the loop below."""
 
@@ -63,6 +175,11 @@ class OracleBackend:
 
     def detect_language(self, cross):
         return detect_language(self.model, cross, self.model.dims.specials)
+
+    def align(self, cross, sot_sequence, text_tokens, num_frames):
+        dims = self.model.dims
+        return find_alignment(self.model, cross, sot_sequence, text_tokens, dims.specials, num_frames,
+                              dims.default_alignment_heads())
 
 
 def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperatures=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0),
@@ -84,6 +201,7 @@ def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperat
     tok = tokenizer(language)
     sup = list(suppress_tokens) if suppress_tokens is not None else list(tok.suppressed_tokens([-1]))
     seek, all_tokens, reset_since, out = 0, [], 0, []
+    last_speech = 0.0
     while seek < content:
         size = min(3000, content - seek)
         dur = size * 0.01
@@ -125,18 +243,22 @@ def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperat
         cur, seek, single = _split(res.tokens, st.timestamp_begin, toff, size, dur, seek)
         if word_timestamps:
             text_tokens = [t for s in cur for t in s["tokens"] if t < st.eot]
+            al = []
             if text_tokens:
-                probs, ti, tj = find_alignment(model, cross, tok.sot_sequence, text_tokens, st, size,
-                                               dims.default_alignment_heads())
-                for s in cur:
-                    s["alignment"] = (probs, ti, tj)
+                probs, ti, tj = be.align(cross, tok.sot_sequence, text_tokens, size)
+                al = words_from_alignment(tok, text_tokens, probs, ti, tj)
+            last_speech = add_word_timestamps([cur], tok, [al], last_speech)
+            if not single:
+                lw = last_word_end(cur)
+                if lw is not None and lw > toff:
+                    seek = round(lw * 100)
         for s in cur:
             text = tok.decode(s["tokens"])
             if s["start"] == s["end"] or not text.strip():
                 continue
             all_tokens.extend(s["tokens"])
             out.append(dict(start=s["start"], end=s["end"], text=text, tokens=s["tokens"], avg_logprob=alp,
-                            no_speech_prob=res.no_speech_prob, temperature=T))
+                            no_speech_prob=res.no_speech_prob, temperature=T, words=s.get("words")))
         if not condition_on_previous_text or T > 0.5:
             reset_since = len(all_tokens)
     return out, language

@@ -385,3 +385,31 @@ print(json.dumps(out))
     import json
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["1"] == out["2"] and len(out["1"]) > 0
+
+
+def test_worker_call_throughput_mode(tmp_path, monkeypatch):
+    """VLOG_AMD_THROUGHPUT=1: the unchanged worker's call (compat overlay, vad_filter=True, beam 5) runs through
+    BatchedInferencePipeline and still yields timed segments for its WebVTT; on a clip without long pauses the
+    windows are the same 30 s windows, so the text matches the batched pipeline called directly."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "compat"))
+    from faster_whisper import WhisperModel as FWModel
+    from vlog_amd.audio import write_wav
+    from vlog_amd.transcribe import BatchedInferencePipeline
+    from vlog_amd.vtt import generate_webvtt
+    monkeypatch.setenv("VLOG_AMD_THROUGHPUT", "1")
+    model = FWModel("synthetic:tiny:3", device="cpu", compute_type="int8", eot_after=60)
+    assert model.throughput
+    wav = tmp_path / "t.wav"
+    x = np.concatenate([speech_like(30.0, 360 + i) for i in range(3)])
+    write_wav(str(wav), x)
+    segments, info = model.transcribe(str(wav), language=None, task="transcribe", beam_size=5, vad_filter=True,
+                                      temperature=0.0)
+    seg_list = [{"start": s.start, "end": s.end, "text": s.text} for s in segments]
+    vtt = generate_webvtt(seg_list)
+    assert seg_list and vtt.count(" --> ") == len(seg_list)
+    assert all(a["start"] <= b["start"] for a, b in zip(seg_list, seg_list[1:]))
+    direct, _ = BatchedInferencePipeline(model).transcribe(str(wav), language=info.language, beam_size=5, vad_filter=True,
+                                                           temperature=0.0, without_timestamps=False)
+    assert [s["text"] for s in seg_list] == [s.text for s in direct]

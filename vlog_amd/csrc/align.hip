@@ -97,9 +97,9 @@ __global__ void align_median_kernel(const float* __restrict__ z, int S, int nh, 
 }
 
 // cost [(N+1)][(M+1)] f32, trace [(N+1)][(M+1)] int8 scratch; x [N][M]; out path (text, time) reversed order fixed
-__global__ __launch_bounds__(256) void dtw_kernel(const float* __restrict__ x, int N, int M, float* __restrict__ cost,
-                                                  signed char* __restrict__ trace, int* __restrict__ out_i,
-                                                  int* __restrict__ out_j, int* __restrict__ out_len) {
+__device__ __forceinline__ void dtw_kernel_body(const float* __restrict__ x, int N, int M, float* __restrict__ cost,
+                                                signed char* __restrict__ trace, int* __restrict__ out_i,
+                                                int* __restrict__ out_j, int* __restrict__ out_len) {
   const int tid = threadIdx.x;
   const long long W = M + 1;
   for (long long k = tid; k < (long long)(N + 1) * W; k += 256) {
@@ -145,6 +145,12 @@ __global__ __launch_bounds__(256) void dtw_kernel(const float* __restrict__ x, i
   }
 }
 
+__global__ __launch_bounds__(256) void dtw_kernel(const float* __restrict__ x, int N, int M, float* __restrict__ cost,
+                                                  signed char* __restrict__ trace, int* __restrict__ out_i,
+                                                  int* __restrict__ out_j, int* __restrict__ out_len) {
+  dtw_kernel_body(x, N, M, cost, trace, out_i, out_j, out_len);
+}
+
 void launch_token_probs(const float* logits, int rows, int V, int eot, const int* next_tok, float* out, hipStream_t st) {
   if (rows <= 0) return;
   hipLaunchKernelGGL(token_probs_kernel, dim3(rows), dim3(256), 0, st, logits, V, eot, next_tok, out);
@@ -166,4 +172,27 @@ void launch_dtw(const float* x, int N, int M, float* cost, signed char* trace, i
                 hipStream_t st) {
   hipLaunchKernelGGL(dtw_kernel, dim3(1), dim3(256), 0, st, x, N, M, cost, trace, out_i, out_j, out_len);
   WM_LAUNCH_CHECK("dtw_kernel");
+}
+
+// Batched DTW: one workgroup per matrix (item b reads x + x_off[b], an N[b] x M[b] matrix; its cost / trace
+// scratch starts at c_off[b], (N+1) x (M+1) cells; its path goes to out + p_off[b], capacity N + M).  The same
+// wavefront and backtrace as dtw_kernel, so every item's path is bit-identical to a dtw_kernel launch on it.
+__global__ __launch_bounds__(256) void dtw_batch_kernel(const float* __restrict__ x, const long long* __restrict__ x_off,
+                                                        const int* __restrict__ Ns, const int* __restrict__ Ms,
+                                                        float* __restrict__ cost_all, signed char* __restrict__ trace_all,
+                                                        const long long* __restrict__ c_off, int* __restrict__ out_i,
+                                                        int* __restrict__ out_j, const long long* __restrict__ p_off,
+                                                        int* __restrict__ out_len) {
+  const int b = blockIdx.x;
+  dtw_kernel_body(x + x_off[b], Ns[b], Ms[b], cost_all + c_off[b], trace_all + c_off[b], out_i + p_off[b],
+                  out_j + p_off[b], out_len + b);
+}
+
+void launch_dtw_batch(const float* x, const long long* x_off, const int* Ns, const int* Ms, float* cost,
+                      signed char* trace, const long long* c_off, int* out_i, int* out_j, const long long* p_off,
+                      int* out_len, int n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(dtw_batch_kernel, dim3(n), dim3(256), 0, st, x, x_off, Ns, Ms, cost, trace, c_off, out_i, out_j,
+                     p_off, out_len);
+  WM_LAUNCH_CHECK("dtw_batch_kernel");
 }

@@ -52,6 +52,8 @@ void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, con
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
 void launch_dtw(const float*, int, int, float*, signed char*, int*, int*, int*, hipStream_t);
+void launch_dtw_batch(const float*, const long long*, const int*, const int*, float*, signed char*, const long long*,
+                      int*, int*, const long long*, int*, int, hipStream_t);
 
 // Kernel classes timed by the built-in profiler (wm_profile / wm_profile_read).
 enum ProfClass {
@@ -168,7 +170,7 @@ struct wm_engine {
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
   std::vector<DecLayerW> dec_w;
-  DevBuf a_logits, a_attn, a_next, a_probs, a_rowsum, a_z, a_mat, a_cost, a_trace, a_pi, a_pj, a_plen;
+  DevBuf a_logits, a_attn, a_next, a_probs, a_rowsum, a_z, a_mat, a_cost, a_trace, a_pi, a_pj, a_plen, a_meta;
   DevBuf prof_dbytes;        // device counters (attention kernels add the bytes they actually read)
   hipEvent_t ev_get() {
     if (ev_pool.empty()) {
@@ -899,15 +901,16 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   if (a->h_steps) a->h_steps[0] = steps;
 }
 
+// logit_rows (optional): the pass rows whose logits are wanted, in output order (overrides last_only)
 void forward(wm_engine* e, int n_seq, const int* h_slots, int S, const int* h_tokens, float* d_logits, int last_only,
-             const int* h_align, int n_align, float* d_attn, hipStream_t st) {
+             const int* h_align, int n_align, float* d_attn, hipStream_t st, const std::vector<int>* logit_rows = nullptr) {
   check_weights(e);
   const auto& m = e->dm;
   const int C = m.n_text_ctx, H = m.n_head;
   if (S <= 0 || S > C) throw std::runtime_error("forward: bad seq_len");
   reserve(e, e->n_slots, n_seq);
   const int rows = n_seq * S;
-  const int nlog = last_only ? n_seq : rows;
+  const int nlog = logit_rows ? (int)logit_rows->size() : last_only ? n_seq : rows;
   ensure_step(e, rows, 1);
   std::vector<int> rt(rows), rp(rows), rh(rows), lr(nlog), hs(n_seq), lin((size_t)n_seq * C);
   for (int s = 0; s < n_seq; ++s) {
@@ -919,7 +922,7 @@ void forward(wm_engine* e, int n_seq, const int* h_slots, int S, const int* h_to
     }
     for (int p = 0; p < C; ++p) lin[(size_t)s * C + p] = s;
   }
-  for (int i = 0; i < nlog; ++i) lr[i] = last_only ? i * S + S - 1 : i;
+  for (int i = 0; i < nlog; ++i) lr[i] = logit_rows ? (*logit_rows)[i] : last_only ? i * S + S - 1 : i;
   std::vector<std::vector<int>> amap(m.n_dec_layer, std::vector<int>(H, -1));
   for (int i = 0; i < n_align; ++i) {
     const int l = h_align[2 * i], h = h_align[2 * i + 1];
@@ -989,6 +992,118 @@ void align(wm_engine* e, int slot, int sot_len, const int* h_sot, int n_text, co
   dtw_run(e, e->a_mat.as<float>(), nrows, F, h_ti, h_tj, h_len, st);
 }
 
+// Batched word alignment (ctranslate2 Whisper.align over a batch of windows [FW↑]): items are chunked so the
+// captured attention (S x heads x 1500 f32 per item) and the text-row logits stay under ~1.5 GB; per chunk ONE
+// teacher-forced decoder pass over every item (sequences padded with <|endoftext|> to the chunk's longest: the
+// pass is causal, so padding never changes a real position), then per item the probabilities and the
+// alignment matrix, and one batched DTW launch for the whole chunk.
+void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int* h_sot, const int* h_text_off,
+                 const int* h_text, const int* h_num_frames, const int* h_heads, int n_heads, int medw, float* h_probs,
+                 const long long* h_path_off, int* h_pi, int* h_pj, int* h_plen, hipStream_t st) {
+  const auto& m = e->dm;
+  const int T = m.n_audio_ctx, V = m.n_vocab;
+  if (n <= 0) return;
+  if (n_heads <= 0) throw std::runtime_error("wm_align_batch: no alignment heads");
+  std::vector<int> S(n), nt(n), F(n);
+  for (int i = 0; i < n; ++i) {
+    nt[i] = h_text_off[i + 1] - h_text_off[i];
+    S[i] = sot_len + 1 + nt[i] + 1;
+    F[i] = h_num_frames[i] / 2;
+    if (nt[i] <= 0 || S[i] > m.n_text_ctx) throw std::runtime_error("wm_align_batch: bad token count");
+    if (F[i] <= 0 || F[i] > T) throw std::runtime_error("wm_align_batch: bad num_frames");
+  }
+  const double budget = 1.5e9;
+  int i0 = 0;
+  while (i0 < n) {
+    int i1 = i0, smax = 0;
+    long long ntext = 0;
+    while (i1 < n) {
+      const int s2 = std::max(smax, S[i1]);
+      const double bytes = (double)(i1 - i0 + 1) * s2 * n_heads * T * 4 + (double)(ntext + nt[i1]) * V * 4;
+      if (i1 > i0 && bytes > budget) break;
+      smax = s2;
+      ntext += nt[i1];
+      ++i1;
+    }
+    const int c = i1 - i0;
+    std::vector<int> toks((size_t)c * smax, m.eot), slots(c), lrows, next;
+    for (int k = 0; k < c; ++k) {
+      const int i = i0 + k;
+      int* t = &toks[(size_t)k * smax];
+      for (int j = 0; j < sot_len; ++j) t[j] = h_sot[j];
+      t[sot_len] = m.no_timestamps;
+      for (int j = 0; j < nt[i]; ++j) {
+        t[sot_len + 1 + j] = h_text[h_text_off[i] + j];
+        lrows.push_back(k * smax + sot_len + j);         // position sot_len + j predicts text token j
+        next.push_back(h_text[h_text_off[i] + j]);
+      }
+      slots[k] = h_slots[i];
+    }
+    e->a_logits.ensure((size_t)ntext * V * 4);
+    e->a_attn.ensure((size_t)c * smax * n_heads * T * 4);
+    forward(e, c, slots.data(), smax, toks.data(), e->a_logits.as<float>(), 0, h_heads, n_heads, e->a_attn.as<float>(), st,
+            &lrows);
+    e->a_next.ensure((size_t)ntext * 4);
+    e->a_probs.ensure((size_t)ntext * 4);
+    HIP_OK(hipMemcpyAsync(e->a_next.p, next.data(), ntext * 4, hipMemcpyHostToDevice, st));
+    launch_token_probs(e->a_logits.as<float>(), (int)ntext, V, m.eot, e->a_next.as<int>(), e->a_probs.as<float>(), st);
+    // alignment matrices of the chunk, packed; DTW scratch and path offsets
+    std::vector<long long> xo(c), co(c), po(c);
+    std::vector<int> Ns(c), Ms(c);
+    long long xt = 0, ct = 0, pt = 0;
+    for (int k = 0; k < c; ++k) {
+      const int i = i0 + k;
+      Ns[k] = nt[i] + 1; Ms[k] = F[i];
+      xo[k] = xt; co[k] = ct; po[k] = pt;
+      xt += (long long)Ns[k] * Ms[k];
+      ct += (long long)(Ns[k] + 1) * (Ms[k] + 1);
+      pt += Ns[k] + Ms[k];
+    }
+    e->a_mat.ensure((size_t)xt * 4);
+    e->a_rowsum.ensure((size_t)smax * n_heads * 4);
+    e->a_z.ensure((size_t)n_heads * smax * T * 4);
+    for (int k = 0; k < c; ++k) {
+      const int i = i0 + k;
+      launch_align_matrix(e->a_attn.as<float>() + (size_t)k * smax * n_heads * T, S[i], n_heads, T, F[i], medw, sot_len,
+                          nt[i] + 1, e->a_rowsum.as<float>(), e->a_z.as<float>(), e->a_mat.as<float>() + xo[k], st);
+    }
+    e->a_cost.ensure((size_t)ct * 4);
+    e->a_trace.ensure((size_t)ct);
+    e->a_pi.ensure((size_t)pt * 4);
+    e->a_pj.ensure((size_t)pt * 4);
+    e->a_plen.ensure((size_t)c * 4);
+    e->a_meta.ensure((size_t)c * (3 * 8 + 2 * 4));
+    char* meta = (char*)e->a_meta.p;
+    long long* d_xo = (long long*)meta;
+    long long* d_co = d_xo + c;
+    long long* d_po = d_co + c;
+    int* d_N = (int*)(d_po + c);
+    int* d_M = d_N + c;
+    HIP_OK(hipMemcpyAsync(d_xo, xo.data(), c * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_co, co.data(), c * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_po, po.data(), c * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_N, Ns.data(), c * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_M, Ms.data(), c * 4, hipMemcpyHostToDevice, st));
+    launch_dtw_batch(e->a_mat.as<float>(), d_xo, d_N, d_M, e->a_cost.as<float>(), e->a_trace.as<signed char>(), d_co,
+                     e->a_pi.as<int>(), e->a_pj.as<int>(), d_po, e->a_plen.as<int>(), c, st);
+    std::vector<int> pi(pt), pj(pt), plen(c);
+    HIP_OK(hipMemcpyAsync(h_probs + h_text_off[i0], e->a_probs.p, ntext * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(pi.data(), e->a_pi.p, pt * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(pj.data(), e->a_pj.p, pt * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(plen.data(), e->a_plen.p, c * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (int k = 0; k < c; ++k) {
+      const int i = i0 + k;
+      h_plen[i] = plen[k];
+      for (int q = 0; q < plen[k]; ++q) {
+        h_pi[h_path_off[i] + q] = pi[po[k] + q];
+        h_pj[h_path_off[i] + q] = pj[po[k] + q];
+      }
+    }
+    i0 = i1;
+  }
+}
+
 template <class F>
 int guarded(wm_engine* e, F&& f) {
   try {
@@ -1056,7 +1171,9 @@ void wm_destroy(wm_engine* e) {
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
                     &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt,
-                    &e->xenc, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml})
+                    &e->xenc, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml, &e->a_logits, &e->a_attn,
+                    &e->a_next, &e->a_probs, &e->a_rowsum, &e->a_z, &e->a_mat, &e->a_cost, &e->a_trace, &e->a_pi,
+                    &e->a_pj, &e->a_plen, &e->a_meta})
     b->release();
   if (e->st2) (void)hipStreamDestroy(e->st2);
   for (hipEvent_t ev : {e->ev_fork, e->ev_mid, e->ev_join})
@@ -1185,6 +1302,19 @@ int wm_align(wm_engine* e, int32_t slot, int32_t sot_len, const int32_t* h_sot, 
     check_weights(e);
     align(e, slot, sot_len, h_sot, n_text, h_text, num_frames, h_heads, n_heads, median_filter_width, h_probs, h_text_idx,
           h_time_idx, h_path_len, (hipStream_t)stream);
+  });
+}
+
+int wm_align_batch(wm_engine* e, int32_t n, const int32_t* h_slots, int32_t sot_len, const int32_t* h_sot,
+                   const int32_t* h_text_off, const int32_t* h_text, const int32_t* h_num_frames, const int32_t* h_heads,
+                   int32_t n_heads, int32_t median_filter_width, float* h_probs, const int64_t* h_path_off,
+                   int32_t* h_text_idx, int32_t* h_time_idx, int32_t* h_path_len, void* stream) {
+  return guarded(e, [&] {
+    check_weights(e);
+    for (int i = 0; i < n; ++i)
+      if (h_slots[i] < 0 || h_slots[i] >= e->n_slots) throw std::runtime_error("wm_align_batch: slot out of range");
+    align_batch(e, n, h_slots, sot_len, h_sot, h_text_off, h_text, h_num_frames, h_heads, n_heads, median_filter_width,
+                h_probs, (const long long*)h_path_off, h_text_idx, h_time_idx, h_path_len, (hipStream_t)stream);
   });
 }
 

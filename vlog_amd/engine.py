@@ -318,6 +318,39 @@ class GpuEngine:
         k = int(n[0])
         return probs[: len(text)], ti[:k].copy(), tj[:k].copy()
 
+    def align_batch(self, slots: Sequence[int], sot_sequence: Sequence[int], texts: Sequence[Sequence[int]],
+                    num_frames: Sequence[int], alignment_heads: Sequence[Tuple[int, int]], median_filter_width: int = 7):
+        """wm_align_batch: CTranslate2 Whisper.align for several windows at once -> one (text_token_probs,
+        text_indices, time_indices) per window (every window needs >= 1 text token)."""
+        n = len(slots)
+        if n == 0:
+            return []
+        sot = np.ascontiguousarray(sot_sequence, dtype=np.int32)
+        lens = [len(t) for t in texts]
+        off = np.zeros(n + 1, dtype=np.int32)
+        off[1:] = np.cumsum(lens)
+        text = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.int32) for t in texts]), dtype=np.int32)
+        nf = np.ascontiguousarray(num_frames, dtype=np.int32)
+        cap = [l + 1 + f // 2 for l, f in zip(lens, nf)]
+        poff = np.zeros(n, dtype=np.int64)
+        poff[1:] = np.cumsum(cap)[:-1]
+        heads = np.ascontiguousarray(np.asarray(alignment_heads, dtype=np.int32).reshape(-1, 2))
+        probs = np.zeros(max(int(off[-1]), 1), dtype=np.float32)
+        ti = np.zeros(sum(cap), dtype=np.int32)
+        tj = np.zeros(sum(cap), dtype=np.int32)
+        plen = np.zeros(n, dtype=np.int32)
+        hs = np.ascontiguousarray(slots, dtype=np.int32)
+        with torch.cuda.device(self.device):
+            _capi.check(self.lib.wm_align_batch(self.h, n, _i32p(hs), len(sot), _i32p(sot), _i32p(off), _i32p(text), _i32p(nf),
+                                                _i32p(heads), heads.shape[0], median_filter_width, _f32p(probs),
+                                                poff.ctypes.data_as(C.POINTER(C.c_int64)), _i32p(ti), _i32p(tj),
+                                                _i32p(plen), self.stream_ptr()), "wm_align_batch")
+        out = []
+        for i in range(n):
+            a, k = int(poff[i]), int(plen[i])
+            out.append((probs[off[i]: off[i + 1]].copy(), ti[a: a + k].copy(), tj[a: a + k].copy()))
+        return out
+
     def dtw(self, cost: torch.Tensor):
         """DTW path of a device cost matrix [N, M] (f32)."""
         cost = cost.to(self.device, torch.float32).contiguous()

@@ -161,8 +161,15 @@ class WhisperModel:
                  compute_type: str = "default", cpu_threads: int = 0, num_workers: int = 1,
                  download_root: Optional[str] = None, local_files_only: bool = False, files: dict = None,
                  revision: Optional[str] = None, use_auth_token=None, seed: int = 0,
-                 eot_after: Optional[int] = None, **model_kwargs):
+                 eot_after: Optional[int] = None, throughput: Optional[bool] = None, **model_kwargs):
+        """throughput: route transcribe() through BatchedInferencePipeline (default: the VLOG_AMD_THROUGHPUT
+        environment variable, so the unchanged worker can opt in without code changes)."""
         from .engine import GpuEngine
+
+        if throughput is None:
+            throughput = os.environ.get("VLOG_AMD_THROUGHPUT", "0") not in ("", "0")
+        self.throughput = bool(throughput)
+        self._batched = None
 
         if files:
             raise NotImplementedError("in-memory model files are not supported")
@@ -188,6 +195,11 @@ class WhisperModel:
         self.input_stride = INPUT_STRIDE
         self.time_precision = TIME_PRECISION
         self.max_length = MAX_LENGTH
+
+    def _pipeline(self) -> "BatchedInferencePipeline":
+        if self._batched is None:
+            self._batched = BatchedInferencePipeline(self, max_batch_windows=int(os.environ.get("VLOG_AMD_BATCH_WINDOWS", "150")))
+        return self._batched
 
     @property
     def is_multilingual(self) -> bool:
@@ -273,6 +285,23 @@ class WhisperModel:
             raise NotImplementedError("chunk_length other than 30 s is not supported")
         if task not in ("transcribe", "translate"):
             raise ValueError(f"unknown task {task!r}")
+        if self.throughput:
+            # opt-in throughput mode for the UNCHANGED worker (VLOG_AMD_THROUGHPUT=1): its call
+            # transcribe(wav, language, task, beam_size=5, vad_filter=True) runs as BatchedInferencePipeline:
+            # VAD-bounded windows decoded independently in large batches (no previous-text prompt), with
+            # timestamps kept so the worker's WebVTT still gets per-segment times.
+            if initial_prompt is not None or clip_timestamps not in ("0", [0], [0.0]) or prefix is not None:
+                raise NotImplementedError("initial_prompt / clip_timestamps / prefix in throughput mode")
+            return self._pipeline().transcribe(
+                audio, language=language, task=task, beam_size=beam_size, best_of=best_of, patience=patience,
+                length_penalty=length_penalty, temperature=temperature,
+                compression_ratio_threshold=compression_ratio_threshold, log_prob_threshold=log_prob_threshold,
+                no_speech_threshold=no_speech_threshold, suppress_blank=suppress_blank, suppress_tokens=suppress_tokens,
+                without_timestamps=without_timestamps, max_initial_timestamp=max_initial_timestamp,
+                word_timestamps=word_timestamps, prepend_punctuations=prepend_punctuations,
+                append_punctuations=append_punctuations, vad_filter=vad_filter, vad_parameters=vad_parameters,
+                max_new_tokens=max_new_tokens, language_detection_threshold=language_detection_threshold,
+                language_detection_segments=language_detection_segments)
         if not isinstance(audio, np.ndarray):
             audio = load_audio(audio)
         audio = np.asarray(audio, dtype=np.float32)
@@ -423,23 +452,27 @@ class WhisperModel:
             segment_size = min(N_FRAMES, content_frames - seek, clip_end - seek)
             segment_duration = segment_size * HOP_LENGTH / SAMPLE_RATE
             previous_tokens = all_tokens[prompt_reset_since:]
+            # one lock scope from the encode to the word alignment: the alignment reads the window's encoder
+            # output from slot 0, which another thread's transcribe must not replace in between
             with self._lock:
                 self._encode(features, seek, segment_size, 0)
                 prompt = self.get_prompt(tokenizer, previous_tokens, options.without_timestamps)
                 result, avg_lp, temperature, cr = self.generate_with_fallback(prompt, tokenizer, options, seed=window)
+                skip = segs.should_skip_window(result.no_speech_prob, avg_lp, options.no_speech_threshold,
+                                               options.log_prob_threshold)
+                if not skip:
+                    previous_seek = seek
+                    current, seek, single_ending = segs.split_segments_by_timestamps(
+                        result.tokens, tokenizer.timestamp_begin, time_offset, segment_size, segment_duration, seek)
+                    if options.word_timestamps:
+                        last_speech_timestamp = self.add_word_timestamps(
+                            [current], tokenizer, segment_size, options.prepend_punctuations,
+                            options.append_punctuations, last_speech_timestamp)
             window += 1
-            if segs.should_skip_window(result.no_speech_prob, avg_lp, options.no_speech_threshold, options.log_prob_threshold):
+            if skip:
                 seek += segment_size
                 continue
-            tokens = result.tokens
-            previous_seek = seek
-            current, seek, single_ending = segs.split_segments_by_timestamps(
-                tokens, tokenizer.timestamp_begin, time_offset, segment_size, segment_duration, seek)
             if options.word_timestamps:
-                with self._lock:
-                    last_speech_timestamp = self.add_word_timestamps(
-                        [current], tokenizer, segment_size, options.prepend_punctuations, options.append_punctuations,
-                        last_speech_timestamp)
                 if not single_ending:
                     last_word_end = _get_end(current)
                     if last_word_end is not None and last_word_end > time_offset:
@@ -458,19 +491,26 @@ class WhisperModel:
                 prompt_reset_since = len(all_tokens)
 
     # ------------------------------------------------------------------ word timestamps
-    def find_alignment(self, tokenizer: Tokenizer, text_tokens: List[List[int]], num_frames: int,
-                       median_filter_width: int = 7, slot: int = 0) -> List[List[dict]]:
+    def find_alignment(self, tokenizer: Tokenizer, text_tokens: List[List[int]], num_frames: Union[int, Sequence[int]],
+                       median_filter_width: int = 7, slots: Optional[Sequence[int]] = None) -> List[List[dict]]:
         """faster-whisper find_alignment over CTranslate2 align: teacher-forced decoder pass over
         [sot_sequence, <|notimestamps|>, text, <|endoftext|>] with the alignment heads' cross-attention
-        captured on the GPU, normalise + median filter + DTW on the GPU (vlog_amd/align.py)."""
-        from .align import align_tokens
+        captured on the GPU, normalise + median filter + DTW on the GPU — every segment group of the call in
+        ONE batched align (wm_align_batch).  Group i reads the encoder output in slot slots[i] (default 0) and
+        num_frames[i] mel frames (an int applies to every group)."""
+        n = len(text_tokens)
+        nfs = list(num_frames) if isinstance(num_frames, (list, tuple, np.ndarray)) else [int(num_frames)] * n
+        sl = list(slots) if slots is not None else [0] * n
+        todo = [i for i in range(n) if text_tokens[i]]
+        aligned = dict(zip(todo, self.engine.align_batch([sl[i] for i in todo], tokenizer.sot_sequence,
+                                                         [text_tokens[i] for i in todo], [nfs[i] for i in todo],
+                                                         self.dims.default_alignment_heads(), median_filter_width)))
         out = []
-        for tt in text_tokens:
+        for i, tt in enumerate(text_tokens):
             if not tt:
                 out.append([])
                 continue
-            probs, text_idx, time_idx = align_tokens(self.engine, self.dims, tokenizer, tt, num_frames,
-                                                     median_filter_width, slot)
+            probs, text_idx, time_idx = aligned[i]
             words, word_tokens = tokenizer.split_to_word_tokens(tt + [tokenizer.eot])
             if len(word_tokens) <= 1:
                 out.append([])
@@ -488,8 +528,12 @@ class WhisperModel:
                         for w, t, s, e, p in zip(words, word_tokens, starts, ends, wprob)])
         return out
 
-    def add_word_timestamps(self, segments: List[List[dict]], tokenizer: Tokenizer, num_frames: int,
-                            prepend_punctuations: str, append_punctuations: str, last_speech_timestamp: float) -> float:
+    def add_word_timestamps(self, segments: List[List[dict]], tokenizer: Tokenizer, num_frames: Union[int, Sequence[int]],
+                            prepend_punctuations: str, append_punctuations: str, last_speech_timestamp: float,
+                            slots: Optional[Sequence[int]] = None) -> float:
+        """faster-whisper add_word_timestamps: segment group i (one window's segments) is aligned against the
+        encoder output in slot slots[i] with num_frames[i] frames (BatchedInferencePipeline passes one group
+        per window of a batch)."""
         if len(segments) == 0:
             return last_speech_timestamp
         text_tokens, per_seg = [], []
@@ -497,7 +541,7 @@ class WhisperModel:
             st = [[t for t in sub["tokens"] if t < tokenizer.eot] for sub in segment]
             text_tokens.append(list(itertools.chain.from_iterable(st)))
             per_seg.append(st)
-        alignments = self.find_alignment(tokenizer, text_tokens, num_frames)
+        alignments = self.find_alignment(tokenizer, text_tokens, num_frames, slots=slots)
         med_max = []
         for alignment in alignments:
             durs = np.array([w["end"] - w["start"] for w in alignment])
@@ -592,6 +636,7 @@ class WindowResult:
     temperature: float
     compression_ratio: float
     no_speech_prob: float
+    segments: Optional[List[dict]] = None      # split (and, with word timestamps, word-aligned) segments
 
 
 class BatchedInferencePipeline:
@@ -604,6 +649,7 @@ class BatchedInferencePipeline:
     def __init__(self, model: WhisperModel, max_batch_windows: int = 150):
         self.model = model
         self.max_batch_windows = max_batch_windows
+        self._last_speech = 0.0
 
     # -- windows of the whole-file feature matrix
     @staticmethod
@@ -683,9 +729,21 @@ class BatchedInferencePipeline:
                     cand = [t for t in tries[i] if t[4]] or tries[i]
                     r, alp, _, cr, _ = max(cand, key=lambda t: t[1])
                     results[i] = (r, alp, options.temperatures[-1], cr)
-            for i, (s, n) in enumerate(wins):
-                r, alp, T, cr = results[i]
-                out.append(WindowResult(b0 + i, s, n, time_offsets[b0 + i], r.tokens, alp, T, cr, r.no_speech_prob))
+                batch = []
+                for i, (s, n) in enumerate(wins):
+                    r, alp, T, cr = results[i]
+                    wr = WindowResult(b0 + i, s, n, time_offsets[b0 + i], r.tokens, alp, T, cr, r.no_speech_prob)
+                    wr.segments = self.window_segments(wr, tokenizer, options)
+                    batch.append(wr)
+                if options.word_timestamps:
+                    # the batch's encoder outputs are still in slots 0..B-1: one batched alignment for every
+                    # window with text (faster-whisper aligns a whole batch of segments in one model.align)
+                    idx = [i for i, wr in enumerate(batch) if wr.segments]
+                    if idx:
+                        self._last_speech = m.add_word_timestamps(
+                            [batch[i].segments for i in idx], tokenizer, [batch[i].size for i in idx],
+                            options.prepend_punctuations, options.append_punctuations, self._last_speech, slots=idx)
+                out.extend(batch)
         return out
 
     def window_segments(self, wr: WindowResult, tokenizer: Tokenizer, options: TranscriptionOptions) -> List[dict]:
@@ -765,6 +823,7 @@ class BatchedInferencePipeline:
             clip_timestamps=clip_timestamps or "0", hallucination_silence_threshold=hallucination_silence_threshold,
             hotwords=hotwords)
         offsets = [s * HOP_LENGTH / SAMPLE_RATE for s, _ in windows]
+        self._last_speech = 0.0
         results = self.decode_windows(features, windows, offsets, tokenizer, options)
         info = TranscriptionInfo(language=language, language_probability=language_probability, duration=duration,
                                  duration_after_vad=duration_after_vad, all_language_probs=all_language_probs,
@@ -772,16 +831,9 @@ class BatchedInferencePipeline:
         return self._segments(features, results, tokenizer, options), info
 
     def _segments(self, features, results: List[WindowResult], tokenizer: Tokenizer, options: TranscriptionOptions):
-        m = self.model
         idx = 0
-        last_speech = 0.0
         for wr in results:
-            cur = self.window_segments(wr, tokenizer, options)
-            if options.word_timestamps and cur:
-                with m._lock:
-                    m._encode(features, wr.seek, wr.size, 0)
-                    last_speech = m.add_word_timestamps([cur], tokenizer, wr.size, options.prepend_punctuations,
-                                                        options.append_punctuations, last_speech)
+            cur = wr.segments if wr.segments is not None else self.window_segments(wr, tokenizer, options)
             for s in cur:
                 text = tokenizer.decode(s["tokens"])
                 if s["start"] == s["end"] or not text.strip():
