@@ -98,6 +98,7 @@ class GenerateOptions:
     sampling_temperature: float = 0.0
     num_hypotheses: int = 1
     seed: int = 0
+    hyp_offset: int = 0        # sampling: index of this window's first hypothesis row in the engine's call
 
 
 def _norm(cum: float, n: int, lp: float) -> float:
@@ -203,18 +204,47 @@ def _beam(model, cross, prompt, st, opt: GenerateOptions) -> GenerateResult:
                           [list(s) for s, _ in ranked])
 
 
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser on uint64 (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def gumbel_noise(seed: int, hyp: int, step: int, V: int) -> np.ndarray:
+    """Counter-based Gumbel noise of the engine's sampling (vlog_amd/csrc/search.hip `gumbel`): for token i,
+    u = ((h >> 40) + 0.5) / 2^24 with h = mix64(seed ^ mix64(hyp << 40 ^ step << 20 ^ i)), g = -log(-log(u)) in
+    float32.  Keyed on (call seed, hypothesis row, decode step, token), so a draw does not depend on batch
+    composition or launch order.  (faster-whisper samples with CTranslate2's own RNG [FW↑]: the draws are
+    this build's, the sampling rule — argmax of logits / T + Gumbel noise = a draw from softmax(logits / T) —
+    is the same.)"""
+    i = np.arange(V, dtype=np.uint64)
+    key = (np.uint64(hyp) << np.uint64(40)) ^ (np.uint64(step) << np.uint64(20)) ^ i
+    h = _mix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ _mix64(key))
+    u = ((h >> np.uint64(40)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+    return -np.log(-np.log(u))
+
+
 def _sample(model, cross, prompt, st, opt: GenerateOptions) -> GenerateResult:
-    rng = np.random.default_rng(opt.seed)
+    """Sampling at temperature T (faster-whisper best_of = num_hypotheses): Gumbel-max over the rule-masked
+    logits / T with the engine's counter-based noise; the best hypothesis by cum_logprob / len**lp."""
     results = []
-    for _ in range(max(1, opt.num_hypotheses)):
+    for j in range(max(1, opt.num_hypotheses)):
         last_logits, cache, no_speech = _prefill(model, cross, prompt, st)
         sampled, cum, pos = [], 0.0, len(prompt)
+        step = 0
         while pos < opt.max_length:
             x = apply_rules(last_logits, sampled, st, opt.suppress_tokens, opt.suppress_blank,
                             opt.max_initial_timestamp_index, opt.with_timestamps)
             lp = log_softmax(x)
-            p = np.exp(log_softmax(x / opt.sampling_temperature))
-            tok = int(rng.choice(len(p), p=p / p.sum()))
+            keys = x / opt.sampling_temperature + gumbel_noise(opt.seed, opt.hyp_offset + j, step, x.shape[0])
+            tok = int(np.argmax(keys))
+            step += 1
             cum += float(lp[tok])
             if tok == st.eot:
                 break

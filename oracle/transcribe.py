@@ -5,8 +5,8 @@ the call the reference worker makes (`worker/transcription.py:105-111`), restate
 product's host code (vlog_amd/transcribe.py) so tests can compare the two end to end:
 seek loop over 30 s windows, <|startofprev|> prompt of the last 223 tokens, temperature fallback on
 compression ratio / avg log-prob with the no-speech exemption, skip on no_speech_prob, segment split at
-timestamp pairs, optional word timestamps.  Sampling temperatures use numpy's RNG, so only the T = 0
-path is expected to match token for token.
+timestamp pairs, optional word timestamps.  Sampling uses the engine's counter-based Gumbel noise
+(oracle/decode.py gumbel_noise), keyed on (window index + temperature index, hypothesis, step, token).
 """
 from __future__ import annotations
 
@@ -202,6 +202,7 @@ def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperat
     sup = list(suppress_tokens) if suppress_tokens is not None else list(tok.suppressed_tokens([-1]))
     seek, all_tokens, reset_since, out = 0, [], 0, []
     last_speech = 0.0
+    window = 0                                  # seeds: window index + temperature index (vlog_amd seeding)
     while seek < content:
         size = min(3000, content - seek)
         dur = size * 0.01
@@ -214,7 +215,7 @@ def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperat
         for i, T in enumerate(temperatures):
             opt = GenerateOptions(beam_size=beam_size if T == 0 else 1, patience=1.0, length_penalty=1.0, max_length=448,
                                   suppress_tokens=sup, suppress_blank=True, max_initial_timestamp_index=50,
-                                  sampling_temperature=T, num_hypotheses=5 if T > 0 else 1, seed=i)
+                                  sampling_temperature=T, num_hypotheses=5 if T > 0 else 1, seed=window + i)
             res = be.generate(cross, prompt, opt)
             n = len(res.tokens)
             alp = res.score * n / (n + 1)
@@ -237,6 +238,7 @@ def transcribe(model, tokenizer, audio: np.ndarray, beam_size: int = 5, temperat
             best = max(below or results, key=lambda x: x[1])
             r = (best[0], best[1], T, best[3])
         res, alp, T, cr = r
+        window += 1
         if res.no_speech_prob > 0.6 and not alp > -1.0:
             seek += size
             continue

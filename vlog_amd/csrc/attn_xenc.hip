@@ -291,14 +291,15 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
     }
     // the NW partials -> the full S^T in every wave: partials to LDS; wave w sums registers
     // [w RPW, (w+1) RPW) over the waves in a fixed order (0..NW-1); every wave reads the 16 sums back
-    constexpr int RPW = 16 / NW;
     if (!(a.abl & 2)) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sX[(wv * 16 + r) * 64 + lane] = sc[r];
       __syncthreads();
+      // wave w sums registers r = w, w + NW, ... over the waves in order 0..NW-1 (any NW)
 #pragma unroll
-      for (int k = 0; k < RPW; ++k) {
-        const int r = wv * RPW + k;
+      for (int k = 0; k < (16 + NW - 1) / NW; ++k) {
+        const int r = wv + k * NW;
+        if (r >= 16) break;
         float v = sX[r * 64 + lane];
 #pragma unroll
         for (int w2 = 1; w2 < NW; ++w2) v += sX[(w2 * 16 + r) * 64 + lane];
@@ -601,7 +602,11 @@ void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const in
     case 512: if (form) { XA_LAUNCH(128, 4, 2); } else { XA_LAUNCH(64, 8, 1); } break;
     case 768: if (form) { XA_LAUNCH(192, 4, 2); } else { XA_LAUNCH(96, 8, 1); } break;
     case 1024: if (form) { XA_LAUNCH(256, 4, 2); } else { XA_LAUNCH(128, 8, 1); } break;
-    case 1280: if (form) { XA_LAUNCH(320, 4, 2); } else { XA_LAUNCH(160, 8, 1); } break;
+    case 1280:
+      if (form == 2) { XA_LAUNCH(128, 10, 2); }          // 10 waves x 128 columns, two tiles staged ahead
+      else if (form) { XA_LAUNCH(320, 4, 2); }
+      else { XA_LAUNCH(160, 8, 1); }
+      break;
     default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
   }
 #undef XA_LAUNCH

@@ -5,6 +5,8 @@ downloading from the HF Hub (`worker/transcription.py:81-85`).  This engine neve
 `resolve_model()` maps
 
   * a local directory with `config.json` + `model.safetensors` (HF Whisper layout) -> those weights;
+  * a local CTranslate2 directory (`model.bin`, the layout a faster-whisper deployment uses) -> its weights,
+    dequantised to float32 (vlog_amd/ct2.py);
   * a name with `VLOG_AMD_MODEL_DIR_<name>` (or `VLOG_AMD_MODEL_ROOT/<name>`) set -> that directory;
   * `"synthetic:<name>[:seed]"` -> random-init weights of that architecture (there are no real
     checkpoints in this environment; BASELINE.md "Synthetic audio");
@@ -173,6 +175,15 @@ def load_hf_dir(path: str) -> Tuple[ModelDims, Dict[str, torch.Tensor]]:
     return dims, sd
 
 
+def load_model_dir(path: str) -> Tuple[ModelDims, Dict[str, torch.Tensor]]:
+    """A local model directory: CTranslate2 (model.bin) or HF (config.json + *.safetensors)."""
+    if os.path.isfile(os.path.join(path, "model.bin")):
+        from .ct2 import load_ct2_dir
+        dims, sd, _ = load_ct2_dir(path)
+        return dims, sd
+    return load_hf_dir(path)
+
+
 def resolve_model(model_size_or_path: str, seed: int = 0, eot_after: Optional[int] = None
                   ) -> Tuple[ModelDims, Dict[str, torch.Tensor], Optional[str]]:
     """-> (dims, float32 CPU state dict, model directory or None)."""
@@ -185,13 +196,13 @@ def resolve_model(model_size_or_path: str, seed: int = 0, eot_after: Optional[in
         dims = model_dims(name)
         return dims, synthetic_state_dict(dims, seed, eot_after), None
     if os.path.isdir(spec):
-        dims, sd = load_hf_dir(spec)
+        dims, sd = load_model_dir(spec)
         return dims, sd, spec
     env = os.environ.get("VLOG_AMD_MODEL_DIR_" + spec.replace("-", "_").replace(".", "_"))
     root = os.environ.get("VLOG_AMD_MODEL_ROOT")
     for cand in [env, os.path.join(root, spec) if root else None]:
         if cand and os.path.isdir(cand):
-            dims, sd = load_hf_dir(cand)
+            dims, sd = load_model_dir(cand)
             return dims, sd, cand
     raise ValueError(
         f"model {spec!r}: no local weights (set VLOG_AMD_MODEL_DIR_<name> or VLOG_AMD_MODEL_ROOT, pass a "
