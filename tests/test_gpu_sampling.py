@@ -19,7 +19,8 @@ from vlog_amd.tokenizer import Tokenizer
 from vlog_amd.weights import round_bf16, synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
-EPS = 0.02
+EPS = 0.02          # nats: bf16 logit noise at a near-tie of two Gumbel keys
+RULE_EPS = 0.05     # the timestamp-forcing gap is a difference of two log-sum-exps: its noise is larger
 
 
 @pytest.fixture(scope="module")
@@ -56,7 +57,7 @@ def _key_margins(orc, cross, prompt, tokens, st, opt, hyp, ended):
         lpp = log_softmax(xp)
         text_max = float(np.max(lpp[:tb]))
         gap = float(np.logaddexp.reduce(lpp[tb:]) - text_max) if np.isfinite(text_max) else -np.inf
-        branches = [gap > 0] + ([gap <= 0] if abs(gap) <= EPS else [])
+        branches = [gap > 0] + ([gap <= 0] if abs(gap) <= RULE_EPS else [])
         best = -np.inf
         for forced in branches:
             x = xp.copy()
@@ -64,7 +65,7 @@ def _key_margins(orc, cross, prompt, tokens, st, opt, hyp, ended):
                 x[:tb] = -np.inf
             k = x / opt.sampling_temperature + g
             best = max(best, float(k[t] - np.max(k)))
-        out.append(best)
+        out.append((best, gap))
     return np.array(out)
 
 
@@ -92,9 +93,10 @@ def test_sampling_matches_oracle_draws(setup, T):
         same += r.tokens == res[w].tokens
         ended = len(prompt) + len(res[w].tokens) < 120
         # the GPU's pick came from one of the window's nh hypotheses: eps-consistent under that one's noise
-        best = max(float(_key_margins(orc, cross, prompt, res[w].tokens, st, opt, w * nh + j, ended).min())
-                   for j in range(nh))
-        assert best >= -EPS, (w, best)
+        per_j = [_key_margins(orc, cross, prompt, res[w].tokens, st, opt, w * nh + j, ended) for j in range(nh)]
+        j = int(np.argmax([m[:, 0].min() for m in per_j]))
+        k = int(np.argmin(per_j[j][:, 0]))
+        assert per_j[j][k, 0] >= -EPS, (w, j, k, per_j[j][k].tolist(), len(res[w].tokens))
         assert abs(r.no_speech_prob - res[w].no_speech_prob) < 1e-3
     assert same >= W // 2, same          # a near-tied key or forcing decision diverges the rest of a sample
 
