@@ -218,15 +218,15 @@ def _mix64(x: np.ndarray) -> np.ndarray:
 
 def gumbel_noise(seed: int, hyp: int, step: int, V: int) -> np.ndarray:
     """Counter-based Gumbel noise of the engine's sampling (vlog_amd/csrc/search.hip `gumbel`): for token i,
-    u = ((h >> 40) + 0.5) / 2^24 with h = mix64(seed ^ mix64(hyp << 40 ^ step << 20 ^ i)), g = -log(-log(u)) in
-    float32.  Keyed on (call seed, hypothesis row, decode step, token), so a draw does not depend on batch
+    u = ((h >> 41) + 0.5) / 2^23 with h = mix64(seed ^ mix64(hyp << 40 ^ step << 20 ^ i)), g = -log(-log(u)) in
+    float32 (u is exact and strictly inside (0, 1)).  Keyed on (call seed, hypothesis row, decode step, token), so a draw does not depend on batch
     composition or launch order.  (faster-whisper samples with CTranslate2's own RNG [FW↑]: the draws are
     this build's, the sampling rule — argmax of logits / T + Gumbel noise = a draw from softmax(logits / T) —
     is the same.)"""
     i = np.arange(V, dtype=np.uint64)
     key = (np.uint64(hyp) << np.uint64(40)) ^ (np.uint64(step) << np.uint64(20)) ^ i
     h = _mix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ _mix64(key))
-    u = ((h >> np.uint64(40)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+    u = ((h >> np.uint64(41)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 8388608.0)
     return -np.log(-np.log(u))
 
 

@@ -71,6 +71,7 @@ def _key_margins(orc, cross, prompt, tokens, st, opt, hyp, ended):
 
 def test_gumbel_noise_restatement_properties():
     g = gumbel_noise(5, 3, 7, 200000)
+    assert np.all(np.isfinite(g))
     assert g.dtype == np.float32 and abs(float(g.mean()) - 0.5772) < 0.01 and abs(float(g.std()) - 1.2825) < 0.01
     assert np.array_equal(g, gumbel_noise(5, 3, 7, 200000)) and not np.array_equal(g, gumbel_noise(5, 4, 7, 200000))
 

@@ -45,3 +45,14 @@ def test_suppress_blank_and_tokens_first_step():
     logits = np.zeros(51866, dtype=np.float32)
     got = apply_rules(logits, [], ST, (5, 7), True, 50, with_timestamps=False)
     assert np.isinf(got[[ST.blank, ST.eot, 5, 7]]).all() and np.isfinite(got[8])
+
+
+def test_gumbel_noise_is_finite_gumbel():
+    """The counter-based sampling noise (oracle restatement of the engine's): finite for every counter (u stays
+    strictly inside (0, 1)), Gumbel-distributed, and a pure function of (seed, hypothesis, step, token)."""
+    from oracle.decode import gumbel_noise
+    import numpy as np
+    g = np.concatenate([gumbel_noise(s, h, t, 51866) for s in (0, 7) for h in (0, 5) for t in (0, 3, 400)])
+    assert np.all(np.isfinite(g))
+    assert abs(float(g.mean()) - 0.5772) < 0.01 and abs(float(g.std()) - 1.2825) < 0.02
+    assert np.array_equal(gumbel_noise(7, 5, 3, 100), gumbel_noise(7, 5, 3, 1000)[:100])

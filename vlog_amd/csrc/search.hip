@@ -61,7 +61,9 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
 }
 __device__ __forceinline__ float gumbel(unsigned long long seed, int hyp, int step, int i) {
   unsigned long long h = mix64(seed ^ mix64(((unsigned long long)hyp << 40) ^ ((unsigned long long)step << 20) ^ (unsigned long long)i));
-  const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
+  // 23 random bits: (k + 0.5) / 2^23 is exact in float32 and lies in (0, 1) for every k.  (With 24 bits, k = 2^24 - 1
+  // rounded u up to exactly 1.0f and the key to +inf: that token was drawn with certainty, ~0.3 % of steps.)
+  const float u = ((float)(h >> 41) + 0.5f) * (1.0f / 8388608.0f);
   return -logf(-logf(u));
 }
 
