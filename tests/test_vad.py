@@ -46,3 +46,15 @@ def test_collect_and_restore():
     out = list(restore_speech_timestamps(iter(segs), chunks, 16000))
     assert (out[0].start, out[0].end) == (1.2, 5.8)
     assert (out[1].start, out[1].end) == (1.4, 5.2) and out[1].words[1].start == 5.1
+
+
+def test_segment_end_on_chunk_boundary_stays_in_its_chunk():
+    """faster-whisper 1.1 `get_chunk_index(..., is_end=True)`: an end exactly at a chunk's last (collected)
+    sample maps with that chunk's offset, not the next chunk's (which would add the 3 s silence gap)."""
+    chunks = [{"start": 16000, "end": 32000}, {"start": 80000, "end": 96000}]
+    m = SpeechTimestampsMap(chunks, 16000)
+    assert m.get_original_time(1.0, is_end=True) == 2.0            # end of chunk 0 in collected time
+    assert m.get_original_time(1.0) == 5.0                          # a START at that instant belongs to chunk 1
+    segs = [Segment(1, 0, 0.2, 1.0, " a", [1], -0.1, 1.0, 0.0, None, 0.0)]
+    out = list(restore_speech_timestamps(iter(segs), chunks, 16000))
+    assert (out[0].start, out[0].end) == (1.2, 2.0)

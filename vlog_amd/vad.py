@@ -121,12 +121,17 @@ class SpeechTimestampsMap:
             self.chunk_end_sample.append(c["end"] - silent)
             self.total_silence_before.append(silent / sampling_rate)
 
-    def get_chunk_index(self, time: float) -> int:
-        return min(bisect.bisect(self.chunk_end_sample, int(time * self.sampling_rate)), len(self.chunk_end_sample) - 1)
+    def get_chunk_index(self, time: float, is_end: bool = False) -> int:
+        """faster-whisper 1.1: a segment END that falls exactly on a chunk's last sample stays in that chunk
+        (a plain bisect would move it into the next chunk and add the following silence gap to it)."""
+        sample = int(time * self.sampling_rate)
+        if is_end and sample in self.chunk_end_sample:
+            return self.chunk_end_sample.index(sample)
+        return min(bisect.bisect(self.chunk_end_sample, sample), len(self.chunk_end_sample) - 1)
 
-    def get_original_time(self, time: float, chunk_index=None) -> float:
+    def get_original_time(self, time: float, chunk_index=None, is_end: bool = False) -> float:
         if chunk_index is None:
-            chunk_index = self.get_chunk_index(time)
+            chunk_index = self.get_chunk_index(time, is_end)
         return round(self.total_silence_before[chunk_index] + time, self.time_precision)
 
 
@@ -143,5 +148,5 @@ def restore_speech_timestamps(segments: Iterable, chunks: List[dict], sampling_r
             seg.start, seg.end, seg.words = words[0].start, words[-1].end, words
         else:
             seg.start = m.get_original_time(seg.start)
-            seg.end = m.get_original_time(seg.end)
+            seg.end = m.get_original_time(seg.end, is_end=True)
         yield seg
