@@ -56,6 +56,29 @@ int wm_logmel_finalize(wm_engine* e, float* d_mel, int64_t n_frames, int64_t ld,
  * stand-in (faster-whisper's Silero VAD [FW↑], reached via vad_filter=True at worker/transcription.py:110). */
 int wm_frame_energy(wm_engine* e, const float* d_pcm, int64_t n_samples, int32_t frame, float* d_db, void* stream);
 
+/* Silero VAD v5 (16 kHz) network weights, f32 device pointers in PyTorch layouts: STFT basis [258][256],
+ * encoder convs conv_w[i] [out][in][3] with (in, out) = (129,128), (128,64), (64,64), (64,128) and biases
+ * [out], LSTMCell w_ih/w_hh [512][128] (gate order i, f, g, o) and b_ih/b_hh [512], head conv1x1 [128] + [1]. */
+typedef struct wm_vad_weights {
+  const float* stft_basis;
+  const float* conv_w[4];
+  const float* conv_b[4];
+  const float* w_ih;
+  const float* w_hh;
+  const float* b_ih;
+  const float* b_hh;
+  const float* head_w;
+  const float* head_b;
+} wm_vad_weights;
+
+/* Speech probability of each 512-sample window of d_pcm (n_samples a multiple of 512; the caller pads as
+ * faster-whisper's get_speech_timestamps does), replacing faster-whisper 1.1 SileroVADModel.__call__ [FW↑
+ * vad.py] — its batched encoder (each window prefixed with the previous window's last 64 samples, zeros for
+ * the first) and its sequential LSTM decoder with h, c starting at zero.  d_work: 512 * n_samples/512 floats
+ * of scratch; d_probs: n_samples/512 floats. */
+int wm_vad_probs(wm_engine* e, const wm_vad_weights* w, const float* d_pcm, int64_t n_samples, float* d_work,
+                 float* d_probs, void* stream);
+
 /* Encoder, replacing ctranslate2 Whisper.encode(features) [FW↑] (faster-whisper generate_segments).
  * Window b reads mel frames [h_seek[b], h_seek[b]+h_nframes[b]) of d_mel (ld = frames per mel row) and
  * zero-pads to 3000 frames (faster-whisper pad_or_trim).  Output bf16 [B][1500][n_state]. */

@@ -330,7 +330,7 @@ def test_vad_filter_drops_long_silence():
     m = SpeechTimestampsMap(chunks, 16000)
     assert [s.tokens for s in segs] == [p.tokens for p in plain] and segs
     for s, p in zip(segs, plain):
-        assert s.start == m.get_original_time(p.start) and s.end == m.get_original_time(p.end)
+        assert s.start == m.get_original_time(p.start) and s.end == m.get_original_time(p.end, is_end=True)
         assert 0.0 <= s.start <= s.end
 
 

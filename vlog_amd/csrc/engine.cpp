@@ -22,6 +22,7 @@
 #include "../../include/whisper_mi355.h"
 #include "gemm.h"
 #include "search.h"
+#include "vad.h"
 
 // ---- launchers defined in the .hip files
 void launch_logmel(const float*, long long, long long, long long, long long, int, const float*, const float*,
@@ -1292,6 +1293,25 @@ int wm_frame_energy(wm_engine* e, const float* d_pcm, int64_t n_samples, int32_t
     if (frame <= 0) throw std::runtime_error("wm_frame_energy: bad frame size");
     const int frames = (int)((n_samples + frame - 1) / frame);
     launch_frame_energy(d_pcm, n_samples, frame, frames, d_db, (hipStream_t)stream);
+  });
+}
+
+int wm_vad_probs(wm_engine* e, const wm_vad_weights* w, const float* d_pcm, int64_t n_samples, float* d_work,
+                 float* d_probs, void* stream) {
+  return guarded(e, [&] {
+    if (!w || !w->stft_basis || !w->w_ih || !w->w_hh || !w->b_ih || !w->b_hh || !w->head_w || !w->head_b)
+      throw std::runtime_error("wm_vad_probs: missing weight");
+    if (n_samples < 0 || n_samples % 512) throw std::runtime_error("wm_vad_probs: n_samples must be a multiple of 512");
+    VadW vw;
+    vw.basis = w->stft_basis;
+    for (int i = 0; i < 4; ++i) {
+      if (!w->conv_w[i] || !w->conv_b[i]) throw std::runtime_error("wm_vad_probs: missing conv weight");
+      vw.cw[i] = w->conv_w[i];
+      vw.cb[i] = w->conv_b[i];
+    }
+    vw.w_ih = w->w_ih; vw.w_hh = w->w_hh; vw.b_ih = w->b_ih; vw.b_hh = w->b_hh;
+    vw.dec_w = w->head_w; vw.dec_b = w->head_b;
+    launch_vad(vw, d_pcm, n_samples / 512, d_work, d_probs, (hipStream_t)stream);
   });
 }
 

@@ -161,9 +161,13 @@ class WhisperModel:
                  compute_type: str = "default", cpu_threads: int = 0, num_workers: int = 1,
                  download_root: Optional[str] = None, local_files_only: bool = False, files: dict = None,
                  revision: Optional[str] = None, use_auth_token=None, seed: int = 0,
-                 eot_after: Optional[int] = None, throughput: Optional[bool] = None, **model_kwargs):
+                 eot_after: Optional[int] = None, throughput: Optional[bool] = None, vad_model: Optional[str] = None,
+                 **model_kwargs):
         """throughput: route transcribe() through BatchedInferencePipeline (default: the VLOG_AMD_THROUGHPUT
-        environment variable, so the unchanged worker can opt in without code changes)."""
+        environment variable, so the unchanged worker can opt in without code changes).
+        vad_model: Silero VAD v5 weights for vad_filter=True — a local .safetensors/.npz file or
+        "synthetic:<seed>" (default: the VLOG_AMD_SILERO_VAD environment variable; unset = the frame-energy
+        stand-in, vlog_amd/vad.py)."""
         from .engine import GpuEngine
 
         if throughput is None:
@@ -187,6 +191,9 @@ class WhisperModel:
         self.engine = GpuEngine(self.dims, sd, self.device_index)
         del sd
         self.engine.reserve(1, 8)
+        from .silero import SileroVad, default_spec
+        vad_spec = vad_model if vad_model is not None else default_spec()
+        self.vad_net = SileroVad.from_spec(self.engine, vad_spec) if vad_spec else None
         self._lock = threading.RLock()
         self.feature_size = self.dims.n_mels
         self.num_samples_per_token = HOP_LENGTH * INPUT_STRIDE

@@ -3,10 +3,14 @@
 
 faster-whisper runs Silero VAD (ONNX) and then a fixed chunking state machine [FW↑ vad.py
 `get_speech_timestamps`, `collect_chunks`, `restore_speech_timestamps` / `SpeechTimestampsMap`].  The
-state machine, padding and timestamp restoration are restated exactly here.  The Silero network itself is
-not available offline, so the per-512-sample speech probability comes from a GPU frame-energy kernel
-(libwhisper_mi355 `wm_frame_energy`) mapped through a logistic above the file's noise floor — a documented
-stand-in; chunk boundaries therefore do not match Silero's ("parity unpinned").
+state machine, padding and timestamp restoration are restated exactly here.  The per-512-sample speech
+probability comes from
+  * the Silero v5 network on the GPU (vlog_amd/silero.py, libwhisper_mi355 `wm_vad_probs`) when the model was
+    given Silero weights (WhisperModel(vad_model=...) / VLOG_AMD_SILERO_VAD) — on the audio padded exactly as
+    faster-whisper pads it; or
+  * without weights (they are not in this image), a GPU frame-energy kernel (`wm_frame_energy`) mapped through
+    a logistic above the file's noise floor — a documented stand-in whose chunk boundaries do not match
+    Silero's ("parity unpinned").
 """
 from __future__ import annotations
 
@@ -20,6 +24,10 @@ WINDOW = 512
 
 
 def speech_probs(audio: np.ndarray, model) -> np.ndarray:
+    net = getattr(model, "vad_net", None)
+    if net is not None:
+        a = np.asarray(audio, dtype=np.float32)
+        return net(np.pad(a, (0, WINDOW - len(a) % WINDOW)))       # faster-whisper pads a whole window at % == 0
     db = model.engine.frame_energy_db(torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)), WINDOW)
     finite = db[db > -100.0]
     floor = float(np.percentile(finite, 10)) if finite.size else -100.0
