@@ -154,7 +154,7 @@ def composite_roofline(dims, lengths, steps: int, prompt_len: int, elapsed_per_s
     return out
 
 
-def parity_sample(dims, sd, pipe, n_sample: int = 8) -> dict:
+def parity_sample(dims, sd, pipe, n_sample: int = 8, fp8_cross: bool = False) -> dict:
     """Outside the timed region: sampled windows of the last step, decoded by the CPU oracle (engine numeric
     format) from the GPU's own encoder output.  A window is identical when every GPU token is the oracle's
     argmax (teacher-forced, tests/parity_util.py); non-identical windows are re-decoded by the oracle's greedy
@@ -172,6 +172,9 @@ def parity_sample(dims, sd, pipe, n_sample: int = 8) -> dict:
     opt = GenerateOptions(suppress_tokens=pipe.suppress, max_length=448)
     eps = 0.08                                     # tests/test_gpu_configs.py EPS["large-v3"]
     ident, consistent, margins, ref_txt, hyp_txt = 0, 0, [], [], []
+    if fp8_cross:                                  # the oracle attends over the values the kernel sees
+        from oracle.fp8 import quantize_rows
+        enc = {w: quantize_rows(e)[2] for w, e in enc.items()}
     for w in sorted(enc):
         r = window_parity(orc, enc[w], pipe.prompt, res[w], dims.specials, opt, w, eps=eps)
         ident += r.identical
@@ -236,11 +239,15 @@ def main():
     ap.add_argument("--beam", type=int, default=1)
     ap.add_argument("--eot-after", type=int, default=110)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: profiles/traffic_r02_a.json, "
+                    "or traffic_r02_fp8.json with --cross-fp8)")
+    ap.add_argument("--cross-fp8", action="store_true", help="opt-in fp8 (e4m3) cross memory: not the headline")
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-kernel event timing")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity sample (rank 0, untimed)")
     ap.add_argument("--parity-windows", type=int, default=8)
     args = ap.parse_args()
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r02_a.json")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -257,6 +264,8 @@ def main():
     sd = synthetic_state_dict(dims, seed=0, eot_after=args.eot_after)
     from vlog_amd.engine import GpuEngine
     eng = GpuEngine(dims, sd, local)
+    if args.cross_fp8:
+        eng.set_option("cross_fp8", 1)
     keep_sd = rank == 0 and ((world == 1 and not args.no_cpu_baseline) or not args.no_parity)
     if not keep_sd:
         del sd
@@ -316,7 +325,7 @@ def main():
         pipe.keep_windows = tuple(sample_indices(W, args.parity_windows))
         pipe.step()                                             # untimed: keeps the sampled windows' encoder output
         try:
-            parity = parity_sample(dims, sd, pipe)
+            parity = parity_sample(dims, sd, pipe, fp8_cross=args.cross_fp8)
         except Exception as e:  # reported, never fatal to the GPU measurement
             parity = {"error": str(e)[:300]}
     audio_s = world * W * 30.0 * args.steps
@@ -331,8 +340,10 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": f"{args.model} bf16 {'greedy' if args.beam == 1 else 'beam%d' % args.beam}, timestamps on, "
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16+e4m3-cross" if args.cross_fp8 else "bf16",
+        "data": "synthetic",
+        "config": {"workload": f"{args.model} bf16{' (opt-in fp8 e4m3 cross memory)' if args.cross_fp8 else ''} "
+                               f"{'greedy' if args.beam == 1 else 'beam%d' % args.beam}, timestamps on, "
                                f"{W} x 30 s windows per GPU of the seeded speech-like corpus, window-sharded (config 4)",
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
@@ -368,7 +379,8 @@ def main():
             except Exception:
                 pass
         roof["accounting"] = ("factored cross-attention: algorithmic bytes = each active window's encoder output "
-                              "(L x 1500 x d bf16) + q' per launch, counted in-kernel")
+                              + ("(L x 1500 x d e4m3 + 1500 f32 scales)" if args.cross_fp8 else "(L x 1500 x d bf16)")
+                              + " + q' per launch, counted in-kernel")
         out["roofline"] = roof
         enc_ms = sum(breakdown[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
         enc_fl = sum(breakdown[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))

@@ -52,9 +52,19 @@ int wm_logmel(wm_engine* e, const float* d_pcm, int64_t pcm_offset, int64_t n_sa
 int wm_logmel_finalize(wm_engine* e, float* d_mel, int64_t n_frames, int64_t ld, const uint32_t* d_gmax,
                        const float* h_gmax, float* h_gmax_out, void* stream);
 
+/* Streaming ingest: n s16le samples (the worker's ffmpeg output, received through a pipe into a pinned
+ * buffer and copied to the device) -> f32 x / 32768, faster-whisper decode_audio's conversion.  The caller
+ * then runs wm_logmel on the frames whose window lies inside the samples received so far (vlog_amd/ingest.py). */
+int wm_pcm_from_s16(wm_engine* e, const int16_t* d_src, int64_t n, float* d_dst, void* stream);
+
 /* Per-frame log energy (dB) of ceil(n_samples / frame) frames, the speech-probability input of the VAD
  * stand-in (faster-whisper's Silero VAD [FW↑], reached via vad_filter=True at worker/transcription.py:110). */
 int wm_frame_energy(wm_engine* e, const float* d_pcm, int64_t n_samples, int32_t frame, float* d_db, void* stream);
+
+/* The fp8 cross memory's quantisation (wm_set_option "cross_fp8"), exposed for tests: rows of n_state bf16
+ * values -> OCP e4m3 codes of x * 448 / amax_row (round to nearest even) and scale amax_row / 448 per row
+ * (an all-zero row: zeros, scale 0).  wm_cross_kv applies it to the window slots when cross_fp8 is on. */
+int wm_cross_fp8_quantize(wm_engine* e, const void* d_enc, int64_t rows, uint8_t* d_codes, float* d_scale, void* stream);
 
 /* Silero VAD v5 (16 kHz) network weights, f32 device pointers in PyTorch layouts: STFT basis [258][256],
  * encoder convs conv_w[i] [out][in][3] with (in, out) = (129,128), (128,64), (64,64), (64,128) and biases

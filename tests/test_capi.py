@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _header_symbols():
     text = open(os.path.join(ROOT, "include", "whisper_mi355.h")).read()
-    return sorted(set(re.findall(r"\b(wm_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(wm_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_header_symbols():

@@ -152,6 +152,35 @@ def test_large_v3_beam5_128_windows_vs_oracle(lv3):
                                 "steps": steps, "windows": rows}) + "\n")
 
 
+def test_large_v3_fp8_cross_memory_150_windows_vs_oracle(lv3):
+    """Opt-in fp8 cross memory at the bench size: the quantiser bit-exact at n_state 1280, then 150 windows
+    greedy in fp8 mode vs the oracle on the dequantised encoder output; token agreement with the bf16 mode is
+    recorded (it measures the fp8 approximation, not kernel correctness)."""
+    from oracle import fp8
+    codes, scale = lv3.eng.cross_fp8_quantize(lv3.enc[:2])
+    rc, rs, _ = fp8.quantize_rows(lv3.enc[:2].reshape(-1, lv3.dims.n_state).float().cpu().numpy())
+    assert np.array_equal(scale.cpu().numpy(), rs) and np.array_equal(codes.cpu().numpy(), rc)
+    ref, _ = lv3.greedy()
+    lv3.eng.set_option("cross_fp8", 1)
+    try:
+        res, steps = lv3.greedy()
+    finally:
+        lv3.eng.set_option("cross_fp8", 0)
+    eps = EPS["large-v3"]
+    rows = []
+    for w in sample_indices(lv3.W, 6):
+        deq = fp8.quantize_rows(lv3.enc_window(w))[2]
+        rows.append(window_parity(lv3.orc, deq, lv3.prompt, res[w], lv3.st, lv3.opt(), w, eps=eps))
+    from vlog_amd.metrics import edit_distance
+    same = sum(a.tokens == b.tokens for a, b in zip(res, ref))
+    w_delta = sum(edit_distance(b.tokens, a.tokens) for a, b in zip(res, ref)) / max(1, sum(len(b.tokens) for b in ref))
+    record("large-v3 fp8 cross memory 150 windows", rows, steps=steps, identical_to_bf16_mode=same,
+           token_wer_vs_bf16_mode=w_delta, eps=eps)
+    for r in rows:
+        assert r.min_margin_rule_tie >= -eps, (r.window, r.min_margin_rule_tie, r.worst_step, r.worst_gap)
+        assert abs(r.no_speech_gpu - r.no_speech_oracle) < 1e-3
+
+
 # ------------------------------------------------------------------------------------------ configs 2 and 3
 def test_base_greedy_32_windows_vs_oracle():
     """Config 2: base (multilingual) bf16 greedy, batch 32 x 30 s windows."""

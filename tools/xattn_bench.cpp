@@ -1,52 +1,65 @@
 // Microbenchmark of the factored cross-attention kernel (vlog_amd/csrc/attn_xenc.hip) on the bench shape:
-// large-v3, W windows, one row per window (greedy decode step), all windows live.  Times the kernel per
-// launch with HIP events for several key-split counts and ablations (bit 0: no S MFMAs, bit 1: no
-// cross-wave sum, bit 2: no U phase), and reports the algorithmic encoder-output bytes per second.
+// large-v3, W windows, one row per window (greedy decode step), all windows live, bf16 and fp8 (e4m3) cross
+// memory.  Times the kernel per launch with HIP events for several key-split counts and ablations (bit 0: no S
+// MFMAs, bit 1: no cross-wave sum, bit 2: no U phase, bit 4: no E loads), and reports the algorithmic
+// encoder-output bytes per second.  Usage: xattn_bench [W] [splits...]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 typedef __bf16 bf16;
-void launch_xattn(const bf16*, const bf16*, const int*, const int*, const int*, int, long long, int, int, int, int, int,
-                  bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
+void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int,
+                  int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t,
+                  hipEvent_t);
 void xattn_set_ablation(int);
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 int main(int argc, char** argv) {
   const int W = argc > 1 ? atoi(argv[1]) : 150, H = 20, T = 1500, d = 1280, iters = 20;
+  std::vector<int> split_list;
+  for (int i = 2; i < argc; ++i) split_list.push_back(atoi(argv[i]));
+  if (split_list.empty()) split_list = {3};
   bf16 *enc, *qp, *pu;
-  float* pml;
+  float *pml, *scale;
   int *slot, *rh;
   CK(hipMalloc(&enc, (size_t)W * T * d * 2));
   CK(hipMalloc(&qp, (size_t)W * H * d * 2));
   CK(hipMalloc(&pu, (size_t)16 * W * H * d * 2));
   CK(hipMalloc(&pml, (size_t)16 * W * H * 2 * 4));
+  CK(hipMalloc(&scale, (size_t)W * T * 4));
   CK(hipMalloc(&slot, W * 4));
   CK(hipMalloc(&rh, W * 4));
   std::vector<int> id(W);
   for (int i = 0; i < W; ++i) id[i] = i;
+  std::vector<float> one((size_t)W * T, 0.01f);
   CK(hipMemcpy(slot, id.data(), W * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(rh, id.data(), W * 4, hipMemcpyHostToDevice));
-  CK(hipMemset(enc, 0x3c, (size_t)W * T * d * 2));   // ~0.0117 in bf16: finite scores
+  CK(hipMemcpy(scale, one.data(), one.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemset(enc, 0x3c, (size_t)W * T * d * 2));   // bf16 ~0.0117 / e4m3 0x3c = 1.5: finite scores
   CK(hipMemset(qp, 0x3c, (size_t)W * H * d * 2));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const double bytes = (double)W * T * d * 2;
-  for (int abl : {0, 7, 8, 15}) {
-    xattn_set_ablation(abl);
-    for (int splits : {1, 3, 5}) {
-      for (int i = 0; i < 3; ++i)
-        launch_xattn(qp, enc, slot, rh, nullptr, W, W, 1, H, T, d, splits, pu, pml, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr);
-      CK(hipEventRecord(e0, 0));
-      for (int i = 0; i < iters; ++i)
-        launch_xattn(qp, enc, slot, rh, nullptr, W, W, 1, H, T, d, splits, pu, pml, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr);
-      CK(hipEventRecord(e1, 0));
-      CK(hipEventSynchronize(e1));
-      float ms = 0;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      const double us = 1000.0 * ms / iters;
-      printf("abl %d splits %2d  %8.2f us  %7.1f GB/s (encoder output)\n", abl, splits, us, bytes / (us * 1e-6) / 1e9);
+  for (int f8 = 0; f8 < 2; ++f8) {
+    const double bytes = (double)W * T * d * (f8 ? 1 : 2);
+    for (int abl : {0, 1, 2, 4, 7, 16, 23}) {
+      xattn_set_ablation(abl);
+      for (int splits : split_list) {
+        auto run = [&] {
+          launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, splits, pu, pml, nullptr,
+                       nullptr, 0, nullptr, 0, nullptr, nullptr);
+        };
+        for (int i = 0; i < 3; ++i) run();
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; ++i) run();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = 1000.0 * ms / iters;
+        printf("%s abl %2d splits %2d  %8.2f us  %7.1f GB/s (encoder output)\n", f8 ? "fp8 " : "bf16", abl, splits, us,
+               bytes / (us * 1e-6) / 1e9);
+      }
     }
   }
   return 0;

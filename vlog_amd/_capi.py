@@ -17,7 +17,7 @@ ABI_VERSION = 1
 SYMBOLS = (
     "wm_create", "wm_destroy", "wm_last_error", "wm_abi_version", "wm_set_weight", "wm_weights_complete",
     "wm_logmel", "wm_logmel_finalize", "wm_encode", "wm_reserve", "wm_cross_kv", "wm_generate", "wm_forward",
-    "wm_frame_energy", "wm_vad_probs", "wm_align", "wm_align_batch", "wm_dtw", "wm_device_bytes", "wm_profile_classes", "wm_profile_name", "wm_profile", "wm_profile_select",
+    "wm_frame_energy", "wm_pcm_from_s16", "wm_vad_probs", "wm_cross_fp8_quantize", "wm_align", "wm_align_batch", "wm_dtw", "wm_device_bytes", "wm_profile_classes", "wm_profile_name", "wm_profile", "wm_profile_select",
     "wm_profile_read", "wm_set_option", "wm_encoder_attention",
 )
 
@@ -70,6 +70,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "wm_forward": (C.c_int, [vp, i32, C.POINTER(i32), i32, C.POINTER(i32), vp, i32, C.POINTER(i32), i32, vp, vp]),
         "wm_frame_energy": (C.c_int, [vp, vp, i64, i32, vp, vp]),
         "wm_vad_probs": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
+        "wm_pcm_from_s16": (C.c_int, [vp, vp, i64, vp, vp]),
+        "wm_cross_fp8_quantize": (C.c_int, [vp, vp, i64, vp, vp, vp]),
         "wm_align": (C.c_int, [vp, i32, i32, C.POINTER(i32), i32, C.POINTER(i32), i32, C.POINTER(i32), i32, i32,
                                C.POINTER(C.c_float), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), vp]),
         "wm_align_batch": (C.c_int, [vp, i32, C.POINTER(i32), i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),

@@ -178,7 +178,8 @@ __global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
 // ------------------------------------------------------------------------------------------------------
 struct XAttnArgs {
   const bf16* qp;                        // [rows][H][d], pre-scaled (log2 units)
-  const bf16* enc;                       // [slots][T][d]
+  const bf16* enc;                       // [slots][T][d] bf16, or (F8) [slots][T][d] OCP e4m3 bytes
+  const float* escale;                   // F8: [slots][T] per-position scale (E[t] = e4m3[t] * escale[t])
   const int* hyp_slot; const int* row_hyp; const int* done;
   int H, T, d, G, n_mt, splits, n_items, per_xcd;
   long long slab_rows;                   // rows of the whole pass: partial slab stride
@@ -189,21 +190,15 @@ struct XAttnArgs {
   int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0): bit 0 skips
                                          // the S MFMAs, bit 1 the cross-wave sum, bit 2 the U phase, bit 3
                                          // loads E with plain loads (same-box bench: 1 % slower than
-                                         // non-temporal ones; tools/gpu_ablib.sh)
+                                         // non-temporal ones; tools/gpu_ablib.sh), bit 4 skips the E loads
 };
 
-template <int QW, int NW, int DEPTH>
-__global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
-  constexpr int KS = QW / 16, CT = QW / 32, LDR = xldr(QW), CPR = QW / 8;
-  __shared__ __attribute__((aligned(16))) char smem[NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4];
+// One work item: rows of group `grp` x (row, head) m-tile `mt`, key tiles [tb, te) written as partial `split`.
+template <int QW, int NW, int DEPTH, bool F8>
+__device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, int grp, int mt, int split, int tb,
+                                              int te) {
+  constexpr int KS = QW / 16, CT = QW / 32, LDR = xldr(QW), CPR = F8 ? QW / 16 : QW / 8, LS = F8 ? KS / 2 : KS;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
-  // XCD-aware item order: the blocks of one (group, split), i.e. its m-tiles, run on one XCD at about the
-  // same time, so the 2nd..n-th reads of an E tile hit that XCD's L2
-  const int item = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
-  if (item >= a.n_items) return;
-  const int mt = item % a.n_mt;
-  const int rest = item / a.n_mt;
-  const int split = rest % a.splits, grp = rest / a.splits;
   const int M = a.G * a.H;
   const int m = mt * 32 + l32;
   const int row0 = grp * a.G;
@@ -217,10 +212,10 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   }
   if (!__any(valid)) return;             // identical in all waves: uniform exit before any barrier
   const int slot = a.hyp_slot[a.row_hyp[row0]];
-  const int n_tiles = (a.T + 31) / 32;
-  const int tb = split * n_tiles / a.splits, te = (split + 1) * n_tiles / a.splits;
   const int cb = wv * QW;
-  const bf16* E = a.enc + (long long)slot * a.T * a.d + cb;
+  constexpr int EB = F8 ? 1 : 2;                         // bytes per stored E element
+  const char* E = (const char*)a.enc + ((long long)slot * a.T * a.d + cb) * EB;
+  const float* Es = F8 ? a.escale + (long long)slot * a.T : nullptr;
   bf16* sE = (bf16*)smem + wv * 32 * LDR;
   float* sX = (float*)(smem + NW * 32 * LDR * 2);        // [NW][16][64] S^T partials
   float* sRed = sX + NW * 16 * 64;                       // [16][64] their sums
@@ -229,7 +224,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
     if (a.stat && tid == 0) {
       const long long npos = (long long)min(te * 32, a.T) - tb * 32;
       unsigned long long by = nq * (unsigned long long)a.d * 2;
-      if (mt == 0) by += (unsigned long long)(npos * a.d * 2);
+      if (mt == 0) by += (unsigned long long)(npos * a.d * EB + (F8 ? npos * 4 : 0));
       atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), by);
     }
   }
@@ -247,16 +242,27 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 
   // Address arithmetic is recomputed from an opaque copy of the lane id inside the loop (`lo`), so the
   // compiler does not hoist ~40 loop-invariant addresses into registers the accumulators need.
-  i32x4 stgA[KS], stgB[KS];
-  auto load = [&](i32x4 (&stg)[KS], int tile, int lo) {
+  i32x4 stgA[LS], stgB[LS];
+  float scA = 1.f, scB = 1.f;            // F8: lane l (< 32) stages the scale of position tile*32 + l
+  auto load = [&](i32x4 (&stg)[LS], float& scl, int tile, int lo) {
+    if (a.abl & 16) {                    // ablation: no E loads (compute-only timing)
 #pragma unroll
-    for (int i = 0; i < KS; ++i) {
+      for (int i = 0; i < LS; ++i) stg[i] = i32x4{0x3c003c00 + lo, 0x3c003c00, 0x3c003c00, 0x3c003c00 + tile};
+      scl = 1.f;
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < LS; ++i) {
       const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
       const int t = min(tile * 32 + r, a.T - 1);
-      if (a.abl & 8) stg[i] = *(const i32x4*)(E + (long long)t * a.d + ch * 8);
-      else stg[i] = __builtin_nontemporal_load((const i32x4*)(E + (long long)t * a.d + ch * 8));
+      const i32x4* src = (const i32x4*)(E + ((long long)t * a.d) * EB + ch * 16);
+      if (a.abl & 8) stg[i] = *src;
+      else stg[i] = __builtin_nontemporal_load(src);
     }
+    if (F8) scl = Es[min(tile * 32 + (lo & 31), a.T - 1)];
   };
+  float* sScale = nullptr;
+  if (F8) sScale = (float*)(smem + NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4) + wv * 32;
   float* pr_row = nullptr;
   if (a.probs && wv == 0 && valid) {
     const int hm = a.head_map[hd];
@@ -264,16 +270,39 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   }
   // one tile: its staged registers -> the wave's LDS image, the loads of tile + DEPTH into the same
   // registers, then S^T, the cross-wave sum, the online softmax and U^T
-  auto tile_step = [&](int tile, i32x4 (&stg)[KS]) {
+  auto tile_step = [&](int tile, i32x4 (&stg)[LS], float& scl) {
     int lo = lane;
     asm volatile("" : "+v"(lo));
-    // wave-private LDS image of this tile (this wave's earlier reads of it are complete: LDS is in order)
+    // wave-private LDS image of this tile (this wave's earlier reads of it are complete: LDS is in order);
+    // F8: each 16-B chunk of 16 e4m3 values becomes two bf16 chunks (exact: e4m3 is a subset of bf16)
+    int r = lo / CPR, ch = lo % CPR;     // chunk (r, ch) of load i, stepped like the global offsets
 #pragma unroll
-    for (int i = 0; i < KS; ++i) {
-      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
-      *(i32x4*)(sE + r * LDR + 8 * xchunk(r, ch)) = stg[i];
+    for (int i = 0; i < LS; ++i) {
+      if (i) {
+        ch += 64 % CPR;
+        r += 64 / CPR;
+        if (ch >= CPR) { ch -= CPR; ++r; }
+      }
+      if (F8) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int word = stg[i][2 * hf + j];
+            const auto f01 = __builtin_amdgcn_cvt_pk_f32_fp8(word, false);
+            const auto f23 = __builtin_amdgcn_cvt_pk_f32_fp8(word, true);
+            v[4 * j] = f2bf(f01[0]); v[4 * j + 1] = f2bf(f01[1]);
+            v[4 * j + 2] = f2bf(f23[0]); v[4 * j + 3] = f2bf(f23[1]);
+          }
+          *(bf16x8*)(sE + r * LDR + 8 * xchunk(r, 2 * ch + hf)) = v;
+        }
+      } else {
+        *(i32x4*)(sE + r * LDR + 8 * xchunk(r, ch)) = stg[i];
+      }
     }
-    if (tile + DEPTH < te) load(stg, tile + DEPTH, lo);
+    if (F8 && lo < 32) sScale[lo] = scl;
+    if (tile + DEPTH < te) load(stg, scl, tile + DEPTH, lo);
     // ---- S^T partial over this wave's columns
     f32x16 sc = xzero16();
     {
@@ -310,6 +339,18 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
       for (int r = 0; r < 16; ++r) sc[r] = sRed[r * 64 + lane];
     }
     const int t0 = tile * 32;
+    float ps[16];                        // F8: the scale of each S^T row this lane holds (U uses p * scale)
+    if (F8) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 sv = *(const f32x4*)(sScale + 8 * g + 4 * hh);
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          ps[4 * g + e2] = sv[e2];
+          sc[4 * g + e2] *= sv[e2];
+        }
+      }
+    }
     if (t0 + 32 > a.T) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
@@ -342,7 +383,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
     for (int r = 0; r < 16; ++r) {
       const float p = __builtin_amdgcn_exp2f(sc[r] - m_run);
       l_run += p;
-      pf[r >> 3][r & 7] = f2bf(p);
+      pf[r >> 3][r & 7] = f2bf(F8 ? p * ps[r] : p);
     }
     // ---- U^T (wave cols) += E^T . P^T.  Transposed read of rows 16 ks + 8 jh + 4 hh + gq, columns
     // 32 c + 16 (G4 & 1) + 4 gp: chunk 4 c + lowc (lowc = 2 (G4 & 1) + (gp >> 1)) is stored at
@@ -366,11 +407,11 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
         }
     }
   };
-  if (tb < te) load(stgA, tb, lane);
-  if (DEPTH == 2 && tb + 1 < te) load(stgB, tb + 1, lane);
+  if (tb < te) load(stgA, scA, tb, lane);
+  if (DEPTH == 2 && tb + 1 < te) load(stgB, scB, tb + 1, lane);
   for (int tile = tb; tile < te; tile += DEPTH) {
-    tile_step(tile, stgA);
-    if (DEPTH == 2 && tile + 1 < te) tile_step(tile + 1, stgB);
+    tile_step(tile, stgA, scA);
+    if (DEPTH == 2 && tile + 1 < te) tile_step(tile + 1, stgB, scB);
   }
   l_run += __shfl_xor(l_run, 32, 64);
   if (valid) {
@@ -395,6 +436,21 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
         *(bf16x4*)(up + (2 * c + (g >> 1)) * kstride + 8 * (g & 1)) = w;
       }
   }
+}
+
+template <int QW, int NW, int DEPTH, bool F8 = false>
+__global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
+  constexpr int LDR = xldr(QW);
+  __shared__ __attribute__((aligned(16))) char smem[NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4 + (F8 ? NW * 32 * 4 : 0)];
+  const int n_tiles = (a.T + 31) / 32;
+  // XCD-aware item order: the blocks of one (group, split), i.e. its m-tiles, run on one XCD at about the
+  // same time, so the 2nd..n-th reads of an E tile hit that XCD's L2
+  const int item = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
+  if (item >= a.n_items) return;
+  const int mt = item % a.n_mt;
+  const int rest = item / a.n_mt;
+  const int split = rest % a.splits, grp = rest / a.splits;
+  xattn_segment<QW, NW, DEPTH, F8>(a, smem, grp, mt, split, split * n_tiles / a.splits, (split + 1) * n_tiles / a.splits);
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -424,6 +480,7 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
   const long long sstride = a.slab_rows * a.H;          // (row, head) pairs per split slab
   float w[MAXS];
   float Mx = -INFINITY, L = 0.f;
+  const int ns = a.splits;
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) w[s] = 0.f;
   {
@@ -432,10 +489,10 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
     const float* ml = a.part_ml + 2 * ((long long)rc * a.H + h);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
-      if (s < a.splits) Mx = fmaxf(Mx, ml[2 * s * sstride]);
+      if (s < ns) Mx = fmaxf(Mx, ml[2 * s * sstride]);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
-      if (s < a.splits) {
+      if (s < ns) {
         w[s] = ml[2 * s * sstride + 1] * __builtin_amdgcn_exp2f(ml[2 * s * sstride] - Mx);
         L += w[s];
       }
@@ -460,7 +517,7 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
       wb[k] = *(const bf16x8*)(w1 + (s0 + k) * 64 * 16);
 #pragma unroll
       for (int sp = 0; sp < MAXS; ++sp)
-        if (sp < a.splits) pv[k][sp] = *(const bf16x8*)(pu + sp * pstride + (s0 + k) * kstride);
+        if (sp < ns) pv[k][sp] = *(const bf16x8*)(pu + sp * pstride + (s0 + k) * kstride);
         else pv[k][sp] = bf16x8{};
     }
 #pragma unroll
@@ -469,7 +526,7 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
       float u[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int sp = 0; sp < MAXS; ++sp)
-        if (sp < a.splits) {
+        if (sp < ns) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) u[i] = fmaf(w[sp], bf2f(pv[k][sp][i]), u[i]);
         }
@@ -516,6 +573,53 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// fp8 cross memory (opt-in, engine option cross_fp8): a window's encoder output stored as OCP e4m3 with one
+// scale per position, E[t] ~= e4m3(E[t] * 448 / amax_t) * (amax_t / 448), amax_t = max_c |E[t][c]| (an all-zero
+// row stores zeros with scale 0).  Halves the bytes xattn streams per layer and step.  One wave per position;
+// lane j converts groups of 4 consecutive columns (v_cvt_pk_fp8_f32, round to nearest even).
+__global__ __launch_bounds__(256) void xquant8_kernel(const bf16* __restrict__ enc, long long rows, int d,
+                                                      unsigned char* __restrict__ out, float* __restrict__ scale) {
+  constexpr int MAXG = 5;                // d <= 1280 = 5 x 64 lanes x 4 columns
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const bf16* x = enc + row * d;
+  float v[MAXG][4];
+  float amax = 0.f;
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g) {
+    const int c = (g * 64 + lane) * 4;
+    if (c < d) {
+      const bf16x4 q = *(const bf16x4*)(x + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[g][e] = bf2f(q[e]);
+        amax = fmaxf(amax, fabsf(v[g][e]));
+      }
+    }
+  }
+  amax = wave_max(amax);
+  const float inv = amax > 0.f ? 448.0f / amax : 0.f;
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g) {
+    const int c = (g * 64 + lane) * 4;
+    if (c < d) {
+      int w = __builtin_amdgcn_cvt_pk_fp8_f32(v[g][0] * inv, v[g][1] * inv, 0, false);
+      w = __builtin_amdgcn_cvt_pk_fp8_f32(v[g][2] * inv, v[g][3] * inv, w, true);
+      *(int*)(out + row * d + c) = w;
+    }
+  }
+  if (lane == 0) scale[row] = amax / 448.0f;
+}
+
+void launch_xquant8(const bf16* enc, long long rows, int d, unsigned char* out, float* scale, hipStream_t st) {
+  if (rows <= 0) return;
+  if (d % 4 != 0 || d > 1280) throw std::runtime_error("xquant8: n_state must be a multiple of 4, <= 1280");
+  hipLaunchKernelGGL(xquant8_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, enc, rows, d, out, scale);
+  WM_LAUNCH_CHECK("xquant8_kernel");
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -570,15 +674,15 @@ static int g_xattn_abl = [] {            // ablation / load-policy experiments (
 }();
 void xattn_set_ablation(int abl) { g_xattn_abl = abl; }
 
-void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const int* row_hyp, const int* done, int rows,
-                  long long slab_rows, int group, int H, int T, int d, int splits, bf16* part_u, float* part_ml,
-                  float* probs, const int* head_map, int n_align, unsigned long long* stat, hipStream_t st,
-                  hipEvent_t ev0, hipEvent_t ev1) {
+void launch_xattn(const bf16* qp, const void* enc, const float* escale, const int* hyp_slot, const int* row_hyp,
+                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, bf16* part_u,
+                  float* part_ml, float* probs, const int* head_map, int n_align, unsigned long long* stat,
+                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
   if (group <= 0 || rows % group != 0) throw std::runtime_error("xattn: rows must be a multiple of the group");
   if (splits < 1 || splits > XMAXS || splits > (T + 31) / 32) throw std::runtime_error("xattn: bad key splits");
   XAttnArgs a{};
-  a.qp = qp; a.enc = enc; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
+  a.qp = qp; a.enc = (const bf16*)enc; a.escale = escale; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
   a.H = H; a.T = T; a.d = d; a.G = group; a.n_mt = (group * H + 31) / 32; a.splits = splits;
   const long long items = (long long)(rows / group) * a.n_mt * splits;
   if (items > (1LL << 30)) throw std::runtime_error("xattn: too many work items");
@@ -591,9 +695,22 @@ void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const in
     const char* e = std::getenv("VLOG_AMD_XFORM");
     return e ? std::atoi(e) : 0;
   }();
-#define XA_LAUNCH(QW_, NW_, DP_)                                                                                \
-  if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a);   \
-  else hipLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_>), grid, dim3(NW_ * 64), 0, st, a);
+#define XA_LAUNCH_F(QW_, NW_, DP_, F8_)                                                                            \
+  if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a);   \
+  else hipLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_>), grid, dim3(NW_ * 64), 0, st, a);
+#define XA_LAUNCH(QW_, NW_, DP_) XA_LAUNCH_F(QW_, NW_, DP_, false)
+  if (escale) {                          // fp8 cross memory: the default forms only
+    switch (d) {
+      case 384: XA_LAUNCH_F(96, 4, 1, true); break;
+      case 512: XA_LAUNCH_F(64, 8, 1, true); break;
+      case 768: XA_LAUNCH_F(96, 8, 1, true); break;
+      case 1024: XA_LAUNCH_F(128, 8, 1, true); break;
+      case 1280: XA_LAUNCH_F(160, 8, 1, true); break;
+      default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
+    }
+    WM_LAUNCH_CHECK("xattn_kernel");
+    return;
+  }
   // form 0 (default): 8 waves x d/8 columns, one tile staged ahead (80 KB of E in flight per CU);
   // form 1 (VLOG_AMD_XFORM=1, experiment): 4 waves x d/4 columns, two tiles ahead (160 KB), which needs
   // more than the 256 architectural VGPRs per lane at d >= 1024 (spills)
@@ -610,12 +727,13 @@ void launch_xattn(const bf16* qp, const bf16* enc, const int* hyp_slot, const in
     default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
   }
 #undef XA_LAUNCH
+#undef XA_LAUNCH_F
   WM_LAUNCH_CHECK("xattn_kernel");
 }
 
 void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long long slab_rows, const bf16* wvb,
-                     const float* bv, const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int H,
-                     int d, int T, float* probs, const int* head_map, int n_align, hipStream_t st) {
+                     const float* bv, const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int group,
+                     int H, int d, int T, float* probs, const int* head_map, int n_align, hipStream_t st) {
   if (rows <= 0) return;
   XCombArgs a{};
   a.part_u = part_u; a.part_ml = part_ml; a.splits = splits; a.slab_rows = slab_rows; a.wvb = wvb; a.bv = bv;

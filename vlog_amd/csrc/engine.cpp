@@ -30,6 +30,7 @@ void launch_logmel(const float*, long long, long long, long long, long long, int
 void launch_logmel_clamp(float*, long long, long long, long long, const unsigned int*, const float*, hipStream_t);
 void launch_ordered_to_float(const unsigned int*, float*, hipStream_t);
 void launch_frame_energy(const float*, long long, int, int, float*, hipStream_t);
+void launch_pcm_s16(const short*, long long, float*, hipStream_t);
 void launch_layernorm(const float*, long long, const int*, int, int, const float*, const float*, bf16*, long long, hipStream_t);
 void launch_embed(const int*, const int*, const bf16*, const float*, float*, int, int, hipStream_t);
 void launch_im2col_conv1(const float*, long long, const int*, const int*, int, int, int, bf16*, hipStream_t);
@@ -45,10 +46,11 @@ void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, co
 void launch_xpack(const bf16*, bf16*, bf16*, int, int, int, hipStream_t);
 void launch_xq(const bf16*, long long, const CrossFuse&, const bf16*, bf16*, int, int, int, hipStream_t);
 int xattn_splits(int, int, int, int, int);
-void launch_xattn(const bf16*, const bf16*, const int*, const int*, const int*, int, long long, int, int, int, int, int,
+void launch_xquant8(const bf16*, long long, int, unsigned char*, float*, hipStream_t);
+void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int,
                   bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, const float*, const int*, const int*, bf16*,
-                     long long, int, int, int, int, float*, const int*, int, hipStream_t);
+                     long long, int, int, int, int, int, float*, const int*, int, hipStream_t);
 
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
@@ -161,7 +163,9 @@ struct wm_engine {
   // holds its encoder output, 3.84 MB for large-v3), 0 = projected cross-KV panels (attn_dec.hip: 245.8 MB
   // per large-v3 window, projected by wm_cross_kv)
   int cross_mode = 1;
-  DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs
+  DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs (cross_fp8: OCP e4m3 bytes)
+  DevBuf xscale;             // cross_fp8: [n_slots][T] f32 per-position scales
+  int cross_fp8 = 0;         // opt-in fp8 cross memory (factored form only; changes numerics, never the default)
   DevBuf xwkt;               // factored: Wk^T per layer and head [L][H][d][64] bf16, packed from dec.ckv.w
   DevBuf xwvb;               // factored: Wv per layer and head in 16-column blocks [L][H][d/16][64][16]
   bool xwkt_ready = false;
@@ -196,7 +200,7 @@ struct wm_engine {
 
   size_t device_bytes() const {
     size_t t = arena.bytes;
-    for (const DevBuf* b : {&e_cols, &e_h1, &e_x, &e_hb, &e_qkv, &e_ao, &e_ff, &ckv, &xenc, &xwkt, &xwvb, &s_qp, &s_pu, &skv, &s_x, &s_hb, &s_q, &s_ao,
+    for (const DevBuf* b : {&e_cols, &e_h1, &e_x, &e_hb, &e_qkv, &e_ao, &e_ff, &ckv, &xenc, &xscale, &xwkt, &xwvb, &s_qp, &s_pu, &skv, &s_x, &s_hb, &s_q, &s_ao,
                             &s_ff, &s_logits, &s_pm, &s_pl, &s_po, &d_tokens, &d_lin, &d_fin_tok})
       t += b->bytes;
     return t;
@@ -562,13 +566,13 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     }
     {
       ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
-      launch_xattn(qp, e->xenc.as<bf16>(), e->d_hyp_slot.as<int>(), row_hyp, done, rows, sl.total_rows, cross_group, H, T,
+      launch_xattn(qp, e->xenc.p, e->cross_fp8 ? e->xscale.as<float>() : nullptr, e->d_hyp_slot.as<int>(), row_hyp, done, rows, sl.total_rows, cross_group, H, T,
                    d, splits, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
     }
     {
       ProfScope ps(e, P_CROSS_COMB, st, 2.0 * rows * d * d, 2.0 * d * d + 2.0 * splits * rows * prow + 2.0 * rows * d);
-      launch_xcomb_vo(pu, pml, splits, sl.total_rows, wv, bv, row_hyp, done, ao, d, rows, H, d, T, probs, hmap, n_align,
-                      st);
+      launch_xcomb_vo(pu, pml, splits, sl.total_rows, wv, bv, row_hyp, done, ao, d, rows, cross_group, H, d, T, probs, hmap,
+                      n_align, st);
     }
   } else {
     const size_t po = (size_t)r0 * H * 16;
@@ -693,8 +697,13 @@ void reserve(wm_engine* e, int n_slots, int n_hyp) {
     // factored mode keeps each window's encoder output (T x d bf16); projected mode its L x 2 K/V panels
     e->ckv.release();
     e->xenc.release();
-    if (e->cross_mode == 1) e->xenc.ensure((size_t)n_slots * T * m.n_state * 2);
-    else e->ckv.ensure((size_t)L * 2 * n_slots * H * T * 64 * 2);
+    e->xscale.release();
+    if (e->cross_mode == 1) {
+      e->xenc.ensure((size_t)n_slots * T * m.n_state * (e->cross_fp8 ? 1 : 2));
+      if (e->cross_fp8) e->xscale.ensure((size_t)n_slots * T * 4);
+    } else {
+      e->ckv.ensure((size_t)L * 2 * n_slots * H * T * 64 * 2);
+    }
     e->n_slots = n_slots;
   }
   if (n_hyp > e->n_hyp_cap) {
@@ -1146,6 +1155,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_MODE")) e->cross_mode = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
     try {
       build_layout(e);
       build_frontend(e, nullptr);
@@ -1172,7 +1182,7 @@ void wm_destroy(wm_engine* e) {
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
                     &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt,
-                    &e->xenc, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml, &e->a_logits, &e->a_attn,
+                    &e->xenc, &e->xscale, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml, &e->a_logits, &e->a_attn,
                     &e->a_next, &e->a_probs, &e->a_rowsum, &e->a_z, &e->a_mat, &e->a_cost, &e->a_trace, &e->a_pi,
                     &e->a_pj, &e->a_plen, &e->a_meta})
     b->release();
@@ -1261,6 +1271,13 @@ int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void*
     if (slot0 < 0 || slot0 + B > e->n_slots) throw std::runtime_error("wm_cross_kv: slots out of range (wm_reserve first)");
     const auto& m = e->dm;
     const int d = m.n_state, T = m.n_audio_ctx;
+    if (e->cross_mode == 1 && e->cross_fp8) {   // factored, fp8: e4m3 image + per-position scales
+      const size_t per = (size_t)T * d;
+      ProfScope ps(e, P_CROSSKV_GEMM, (hipStream_t)stream, 0, 3.0 * B * per + 4.0 * B * T);
+      launch_xquant8((const bf16*)d_enc, (long long)B * T, d, e->xenc.as<unsigned char>() + (size_t)slot0 * per,
+                     e->xscale.as<float>() + (size_t)slot0 * T, (hipStream_t)stream);
+      return;
+    }
     if (e->cross_mode == 1) {   // factored: the slot holds the encoder output itself
       const size_t per = (size_t)T * d;
       ProfScope ps(e, P_CROSSKV_GEMM, (hipStream_t)stream, 0, 2.0 * 2 * B * per);
@@ -1293,6 +1310,19 @@ int wm_frame_energy(wm_engine* e, const float* d_pcm, int64_t n_samples, int32_t
     if (frame <= 0) throw std::runtime_error("wm_frame_energy: bad frame size");
     const int frames = (int)((n_samples + frame - 1) / frame);
     launch_frame_energy(d_pcm, n_samples, frame, frames, d_db, (hipStream_t)stream);
+  });
+}
+
+int wm_pcm_from_s16(wm_engine* e, const int16_t* d_src, int64_t n, float* d_dst, void* stream) {
+  return guarded(e, [&] {
+    if (n < 0) throw std::runtime_error("wm_pcm_from_s16: negative length");
+    launch_pcm_s16((const short*)d_src, n, d_dst, (hipStream_t)stream);
+  });
+}
+
+int wm_cross_fp8_quantize(wm_engine* e, const void* d_enc, int64_t rows, uint8_t* d_codes, float* d_scale, void* stream) {
+  return guarded(e, [&] {
+    launch_xquant8((const bf16*)d_enc, rows, e->dm.n_state, d_codes, d_scale, (hipStream_t)stream);
   });
 }
 
@@ -1370,6 +1400,19 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
+    else if (k == "cross_fp8") {
+      // fp8 (OCP e4m3) cross memory in the factored form; switching re-allocates the window slots (their
+      // contents are dropped: run wm_cross_kv again)
+      const int v = value ? 1 : 0;
+      if (v != e->cross_fp8) {
+        HIP_OK(hipDeviceSynchronize());
+        e->cross_fp8 = v;
+        const int n = e->n_slots;
+        e->n_slots = 0;
+        if (n > 0) reserve(e, n, e->n_hyp_cap);
+        else { e->xenc.release(); e->xscale.release(); }
+      }
+    }
     else if (k == "cross_mode") {
       // switching re-allocates the window slots in the new form (their contents are dropped: run
       // wm_cross_kv again)

@@ -151,3 +151,31 @@ void launch_frame_energy(const float* pcm, long long n, int W, int frames, float
   hipLaunchKernelGGL(frame_energy_kernel, dim3((frames + 3) / 4), dim3(256), 0, st, pcm, n, W, frames, db);
   WM_LAUNCH_CHECK("frame_energy_kernel");
 }
+
+// Streaming ingest: s16le PCM (as the worker's ffmpeg extraction produces it) -> f32 x / 32768, the
+// conversion faster-whisper's decode_audio applies.  8 samples per thread, 16-B loads.
+__global__ void pcm_s16_kernel(const short* __restrict__ src, long long n, float* __restrict__ dst) {
+  const long long i8 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i8 + 8 <= n && ((reinterpret_cast<uintptr_t>(src + i8) & 15) == 0) && ((reinterpret_cast<uintptr_t>(dst + i8) & 15) == 0)) {
+    const i32x4 v = *(const i32x4*)(src + i8);
+    f32x4 lo, hi;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      lo[2 * k] = (float)(short)(v[k] & 0xffff) * (1.0f / 32768.0f);
+      lo[2 * k + 1] = (float)(short)((unsigned)v[k] >> 16) * (1.0f / 32768.0f);
+      hi[2 * k] = (float)(short)(v[2 + k] & 0xffff) * (1.0f / 32768.0f);
+      hi[2 * k + 1] = (float)(short)((unsigned)v[2 + k] >> 16) * (1.0f / 32768.0f);
+    }
+    *(f32x4*)(dst + i8) = lo;
+    *(f32x4*)(dst + i8 + 4) = hi;
+  } else {
+    for (long long i = i8; i < i8 + 8 && i < n; ++i) dst[i] = (float)src[i] * (1.0f / 32768.0f);
+  }
+}
+
+void launch_pcm_s16(const short* src, long long n, float* dst, hipStream_t st) {
+  if (n <= 0) return;
+  const long long threads = (n + 7) / 8;
+  hipLaunchKernelGGL(pcm_s16_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, src, n, dst);
+  WM_LAUNCH_CHECK("pcm_s16_kernel");
+}

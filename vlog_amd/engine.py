@@ -166,6 +166,16 @@ class GpuEngine:
                                                   B, T, self.stream_ptr()), "wm_encoder_attention")
         return out
 
+    def cross_fp8_quantize(self, enc: torch.Tensor):
+        """wm_cross_fp8_quantize on bf16 rows [..., n_state] -> (uint8 codes, f32 scale per row), device tensors."""
+        x = enc.reshape(-1, enc.shape[-1]).contiguous()
+        codes = torch.empty(x.shape, dtype=torch.uint8, device=self.device)
+        scale = torch.empty(x.shape[0], dtype=torch.float32, device=self.device)
+        _capi.check(self.lib.wm_cross_fp8_quantize(self.h, C.c_void_p(x.data_ptr()), x.shape[0],
+                                                    C.c_void_p(codes.data_ptr()), C.c_void_p(scale.data_ptr()),
+                                                    self.stream_ptr()), "wm_cross_fp8_quantize")
+        return codes, scale
+
     def set_option(self, key: str, value: int) -> None:
         """Engine scheduling knob (wm_set_option), e.g. set_option("decode_split", 0)."""
         _capi.check(self.lib.wm_set_option(self.h, key.encode(), int(value)), "wm_set_option")

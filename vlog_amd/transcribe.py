@@ -656,7 +656,7 @@ class BatchedInferencePipeline:
     def __init__(self, model: WhisperModel, max_batch_windows: int = 150):
         self.model = model
         self.max_batch_windows = max_batch_windows
-        self._last_speech = 0.0
+        self._last_speech_by_file: dict = {}
 
     # -- windows of the whole-file feature matrix
     @staticmethod
@@ -685,7 +685,10 @@ class BatchedInferencePipeline:
         return out
 
     def decode_windows(self, features: torch.Tensor, windows: Sequence[Tuple[int, int]], time_offsets: Sequence[float],
-                       tokenizer: Tokenizer, options: TranscriptionOptions, seed: int = 0) -> List[WindowResult]:
+                       tokenizer: Tokenizer, options: TranscriptionOptions, seed: int = 0,
+                       files: Optional[Sequence[int]] = None) -> List[WindowResult]:
+        """files: the source file of each window when windows of several files share batches (transcribe_many):
+        word timestamps then keep one last-speech time per file."""
         m = self.model
         eng = m.engine
         st = m.dims.specials
@@ -744,12 +747,16 @@ class BatchedInferencePipeline:
                     batch.append(wr)
                 if options.word_timestamps:
                     # the batch's encoder outputs are still in slots 0..B-1: one batched alignment for every
-                    # window with text (faster-whisper aligns a whole batch of segments in one model.align)
-                    idx = [i for i, wr in enumerate(batch) if wr.segments]
-                    if idx:
-                        self._last_speech = m.add_word_timestamps(
-                            [batch[i].segments for i in idx], tokenizer, [batch[i].size for i in idx],
-                            options.prepend_punctuations, options.append_punctuations, self._last_speech, slots=idx)
+                    # window with text (faster-whisper aligns a whole batch of segments in one model.align); with
+                    # several files, one call per file so each keeps its own last-speech time
+                    fid = [files[b0 + i] if files is not None else 0 for i in range(len(batch))]
+                    for f in sorted(set(fid)):
+                        idx = [i for i, wr in enumerate(batch) if wr.segments and fid[i] == f]
+                        if idx:
+                            self._last_speech_by_file[f] = m.add_word_timestamps(
+                                [batch[i].segments for i in idx], tokenizer, [batch[i].size for i in idx],
+                                options.prepend_punctuations, options.append_punctuations,
+                                self._last_speech_by_file.get(f, 0.0), slots=idx)
                 out.extend(batch)
         return out
 
@@ -786,13 +793,82 @@ class BatchedInferencePipeline:
                                    ("hallucination_silence_threshold", hallucination_silence_threshold, None)):
             if val != default:
                 raise NotImplementedError(f"{name}={val!r} is not supported by the MI355X engine")
+        prep = self._prepare(audio, language, vad_filter, vad_parameters, language_detection_segments,
+                             language_detection_threshold)
+        tokenizer = self.model.tokenizer(task=task, language=prep["language"])
+        options = self._options(
+            tokenizer, beam_size=beam_size, best_of=best_of, patience=patience, length_penalty=length_penalty,
+            temperature=temperature, compression_ratio_threshold=compression_ratio_threshold,
+            log_prob_threshold=log_prob_threshold, no_speech_threshold=no_speech_threshold,
+            initial_prompt=initial_prompt, suppress_blank=suppress_blank, suppress_tokens=suppress_tokens,
+            without_timestamps=without_timestamps, max_initial_timestamp=max_initial_timestamp,
+            word_timestamps=word_timestamps, prepend_punctuations=prepend_punctuations,
+            append_punctuations=append_punctuations, max_new_tokens=max_new_tokens, clip_timestamps=clip_timestamps)
+        windows = prep["windows"]
+        offsets = [s * HOP_LENGTH / SAMPLE_RATE for s, _ in windows]
+        self._last_speech_by_file = {}
+        results = self.decode_windows(prep["features"], windows, offsets, tokenizer, options)
+        return self._segments(prep["features"], results, tokenizer, options), self._info(prep, options)
+
+    def transcribe_many(self, audios: Sequence[Union[str, BinaryIO, np.ndarray]],
+                        language: Union[None, str, Sequence[Optional[str]]] = None, task: str = "transcribe",
+                        vad_filter: bool = True, vad_parameters=None, language_detection_segments: int = 1,
+                        language_detection_threshold: Optional[float] = 0.5, **kw):
+        """Several files in shared decode batches: the worker transcribes one video at a time
+        (reference worker/transcription.py:496-506), so a short file leaves most of a 150-window batch empty.
+        Here the windows of all files (same task; grouped by language, since the prompt carries it) are packed
+        into the same batches: the files' log-mel matrices are concatenated along time (each normalised with
+        its own global max, as faster-whisper does per file) and every window keeps its file's time offsets.
+        Returns [(segments, info)] per file, in input order; each file's result is what `transcribe` gives for
+        it alone (same windows, prompts and options)."""
+        n = len(audios)
+        langs = list(language) if isinstance(language, (list, tuple)) else [language] * n
+        if len(langs) != n:
+            raise ValueError("one language per file")
+        preps = [self._prepare(a, l, vad_filter, vad_parameters, language_detection_segments,
+                               language_detection_threshold) for a, l in zip(audios, langs)]
+        out: List[Optional[tuple]] = [None] * n
+        self._last_speech_by_file = {}
+        for lang in sorted({p["language"] for p in preps}):
+            files = [i for i, p in enumerate(preps) if p["language"] == lang]
+            tokenizer = self.model.tokenizer(task=task, language=lang)
+            options = self._options(tokenizer, **kw)
+            feats = torch.cat([preps[i]["features"] for i in files], dim=1) if len(files) > 1 else preps[files[0]]["features"]
+            windows, offsets, fids, bases = [], [], [], {}
+            base = 0
+            for i in files:
+                bases[i] = base
+                for s, nf in preps[i]["windows"]:
+                    windows.append((base + s, nf))
+                    offsets.append(s * HOP_LENGTH / SAMPLE_RATE)
+                    fids.append(i)
+                base += preps[i]["features"].shape[1]
+            results = self.decode_windows(feats, windows, offsets, tokenizer, options, files=fids)
+            for i in files:
+                mine = [wr for wr, f in zip(results, fids) if f == i]
+                for wr in mine:                      # seeks relative to the file again
+                    wr.seek -= bases[i]
+                    for sg in wr.segments or []:
+                        sg["seek"] = wr.seek
+                out[i] = (list(self._segments(None, mine, tokenizer, options)), self._info(preps[i], options))
+        return out
+
+    def _prepare(self, audio, language, vad_filter, vad_parameters, language_detection_segments,
+                 language_detection_threshold) -> dict:
+        """One file: PCM, log-mel, its windows (VAD-bounded or fixed) and its language.  `audio` may be an
+        IngestResult (vlog_amd/ingest.py: PCM and log-mel already on the device, computed while streaming)."""
+        from .ingest import IngestResult
         m = self.model
-        if not isinstance(audio, np.ndarray):
-            audio = load_audio(audio)
-        audio = np.asarray(audio, dtype=np.float32)
-        duration = audio.shape[0] / SAMPLE_RATE
-        with m._lock:
-            features = m._features(audio)
+        if isinstance(audio, IngestResult):
+            features, duration = audio.features, audio.duration
+            audio = audio.pcm
+        else:
+            if not isinstance(audio, np.ndarray):
+                audio = load_audio(audio)
+            audio = np.asarray(audio, dtype=np.float32)
+            duration = audio.shape[0] / SAMPLE_RATE
+            with m._lock:
+                features = m._features(audio)
         content = features.shape[1] - 1
         vad_opts = None
         if vad_filter:
@@ -814,28 +890,39 @@ class BatchedInferencePipeline:
                 language, language_probability = "en", 1.0
         else:
             language_probability = 1.0
-        tokenizer = m.tokenizer(task=task, language=language)
+        return dict(features=features, windows=windows, duration=duration, duration_after_vad=duration_after_vad,
+                    vad_opts=vad_opts, language=language, language_probability=language_probability,
+                    all_language_probs=all_language_probs)
+
+    @staticmethod
+    def _options(tokenizer: Tokenizer, beam_size: int = 5, best_of: int = 5, patience: float = 1,
+                 length_penalty: float = 1, temperature=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0),
+                 compression_ratio_threshold: Optional[float] = 2.4, log_prob_threshold: Optional[float] = -1.0,
+                 no_speech_threshold: Optional[float] = 0.6, initial_prompt=None, suppress_blank: bool = True,
+                 suppress_tokens: Optional[List[int]] = [-1], without_timestamps: bool = True,
+                 max_initial_timestamp: float = 1.0, word_timestamps: bool = False,
+                 prepend_punctuations: str = "\"'“¿([{-", append_punctuations: str = "\"'.。,，!！?？:：”)]}、",
+                 max_new_tokens: Optional[int] = None, clip_timestamps=None) -> TranscriptionOptions:
         temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
-        options = TranscriptionOptions(
+        return TranscriptionOptions(
             beam_size=beam_size, best_of=best_of, patience=patience, length_penalty=length_penalty,
-            repetition_penalty=repetition_penalty, no_repeat_ngram_size=no_repeat_ngram_size,
+            repetition_penalty=1, no_repeat_ngram_size=0,
             log_prob_threshold=log_prob_threshold, no_speech_threshold=no_speech_threshold,
             compression_ratio_threshold=compression_ratio_threshold, condition_on_previous_text=False,
-            prompt_reset_on_temperature=0.5, temperatures=temps, initial_prompt=initial_prompt, prefix=prefix,
+            prompt_reset_on_temperature=0.5, temperatures=temps, initial_prompt=initial_prompt, prefix=None,
             suppress_blank=suppress_blank,
             suppress_tokens=list(tokenizer.suppressed_tokens(suppress_tokens)) if suppress_tokens else [],
             without_timestamps=without_timestamps, max_initial_timestamp=max_initial_timestamp,
             word_timestamps=word_timestamps, prepend_punctuations=prepend_punctuations,
-            append_punctuations=append_punctuations, multilingual=multilingual, max_new_tokens=max_new_tokens,
-            clip_timestamps=clip_timestamps or "0", hallucination_silence_threshold=hallucination_silence_threshold,
-            hotwords=hotwords)
-        offsets = [s * HOP_LENGTH / SAMPLE_RATE for s, _ in windows]
-        self._last_speech = 0.0
-        results = self.decode_windows(features, windows, offsets, tokenizer, options)
-        info = TranscriptionInfo(language=language, language_probability=language_probability, duration=duration,
-                                 duration_after_vad=duration_after_vad, all_language_probs=all_language_probs,
-                                 transcription_options=options, vad_options=vad_opts)
-        return self._segments(features, results, tokenizer, options), info
+            append_punctuations=append_punctuations, multilingual=False, max_new_tokens=max_new_tokens,
+            clip_timestamps=clip_timestamps or "0", hallucination_silence_threshold=None, hotwords=None)
+
+    @staticmethod
+    def _info(prep: dict, options: TranscriptionOptions) -> TranscriptionInfo:
+        return TranscriptionInfo(language=prep["language"], language_probability=prep["language_probability"],
+                                 duration=prep["duration"], duration_after_vad=prep["duration_after_vad"],
+                                 all_language_probs=prep["all_language_probs"], transcription_options=options,
+                                 vad_options=prep["vad_opts"])
 
     def _segments(self, features, results: List[WindowResult], tokenizer: Tokenizer, options: TranscriptionOptions):
         idx = 0

@@ -23,11 +23,23 @@ import torch
 WINDOW = 512
 
 
-def speech_probs(audio: np.ndarray, model) -> np.ndarray:
+def speech_probs(audio, model) -> np.ndarray:
+    """audio: float32 numpy array, or a device tensor (streaming ingest keeps the PCM on the GPU)."""
     net = getattr(model, "vad_net", None)
     if net is not None:
+        pad = WINDOW - len(audio) % WINDOW                         # faster-whisper pads a whole window at % == 0
+        if isinstance(audio, torch.Tensor):
+            a = torch.cat([audio.to(net.engine.device, torch.float32), audio.new_zeros(pad, dtype=torch.float32)])
+            out = net.probs_device(a.contiguous())
+            return out.cpu().numpy()
         a = np.asarray(audio, dtype=np.float32)
-        return net(np.pad(a, (0, WINDOW - len(a) % WINDOW)))       # faster-whisper pads a whole window at % == 0
+        return net(np.pad(a, (0, pad)))
+    if isinstance(audio, torch.Tensor):
+        db = model.engine.frame_energy_db(audio.to(torch.float32), WINDOW)
+        finite = db[db > -100.0]
+        floor = float(np.percentile(finite, 10)) if finite.size else -100.0
+        thr = max(floor + 12.0, -55.0)
+        return 1.0 / (1.0 + np.exp(-(db - thr) / 2.0))
     db = model.engine.frame_energy_db(torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)), WINDOW)
     finite = db[db > -100.0]
     floor = float(np.percentile(finite, 10)) if finite.size else -100.0
