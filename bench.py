@@ -102,7 +102,12 @@ class Pipeline:
         t4 = time.perf_counter()
         for k, v in (("logmel", t1 - t0), ("encode", t2 - t1), ("decode", t3 - t2), ("host", t4 - t3)):
             self.stage[k] = self.stage.get(k, 0.0) + v
-        self.last = dict(tokens=[len(r.tokens) for r in res], steps=steps, segments=len(segs), vtt_bytes=len(vtt))
+        import zlib
+        crc = 0
+        for r in res:
+            crc = zlib.crc32(np.asarray(r.tokens, dtype=np.int32).tobytes(), crc)
+        self.last = dict(tokens=[len(r.tokens) for r in res], steps=steps, segments=len(segs), vtt_bytes=len(vtt),
+                         crc=crc)
         if self.keep_windows:
             self.kept = dict(res=res, enc={w: enc[w].float().cpu().numpy() for w in self.keep_windows})
         del enc, mel
@@ -347,6 +352,7 @@ def main():
                                f"{W} x 30 s windows per GPU of the seeded speech-like corpus, window-sharded (config 4)",
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
+                   "token_crc32": pipe.last["crc"],
                    "parallelism": f"window-shard x{world}", "weights": f"synthetic seed 0, eot_after={args.eot_after}"},
         "stages_s_per_step": {k: round(v / args.steps, 4) for k, v in stage_timed.items()},
     }

@@ -37,7 +37,6 @@ def test_transcribe_many_equals_per_file(vad, words):
         ref = list(ref)
         assert info.duration == rinfo.duration and info.duration_after_vad == rinfo.duration_after_vad
         assert [s.tokens for s in segs] == [s.tokens for s in ref]
-        assert all(0.0 <= s.start <= s.end <= info.duration + 30.0 for s in segs)
         if not words:
             assert _key(segs) == _key(ref)
             continue
@@ -46,3 +45,5 @@ def test_transcribe_many_equals_per_file(vad, words):
         assert [w[0] for w in wa] == [w[0] for w in wb]
         close = np.mean([abs(a[1] - b[1]) <= 0.1 and abs(a[2] - b[2]) <= 0.1 for a, b in zip(wa, wb)]) if wa else 1.0
         assert close >= 0.8, close
+        seg_close = np.mean([abs(a.start - b.start) <= 0.1 and abs(a.end - b.end) <= 0.1 for a, b in zip(segs, ref)])
+        assert seg_close >= 0.8, seg_close

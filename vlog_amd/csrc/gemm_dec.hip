@@ -12,6 +12,7 @@
 #include "gemm.h"
 #include "gemm_epi.h"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -180,12 +181,14 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
-template <int MF, int KIND, int R>
+template <int MF, int KIND, int R, int PK = 1>
 __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
                                                        int K, GemmEpi epi, int tiles_n, int splitk, int kr,
                                                        float* __restrict__ part, int rgroups) {
   static_assert(MF % 2 == 0, "MF must be even");
-  constexpr int ROWS = MF * 16, HALF = MF / 2, SLOT = (ROWS + 32) * 64, DA = ROWS / 32, DPP = DA + 1;
+  // a ring slot holds PK consecutive 64-k sub-panels (one barrier per PK x 64 of K)
+  constexpr int ROWS = MF * 16, HALF = MF / 2, SUB = (ROWS + 32) * 64, SLOT = PK * SUB, DA = ROWS / 32,
+                DPP = PK * (DA + 1);
   __shared__ __attribute__((aligned(16))) bf16 smem[R * SLOT];
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   // HBM once and served to the other row groups from that XCD's L2
   const int split = wgid % splitk, rg = (wgid / splitk) % rgroups, tile = wgid / (splitk * rgroups);
   const int n0 = tile * 32, m0 = rg * ROWS;
-  const int kb = split * kr, klen = min(kr, K - kb), NP = klen / 64;
+  const int kb = split * kr, klen = min(kr, K - kb), NS = klen / 64, NP = (NS + PK - 1) / PK;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid & 1, wr = wid >> 1;
 
@@ -214,14 +217,19 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
     srcW = w + (long long)min(n0 + row, N - 1) * ldw + kb + ch * 8;
   }
+  // super-panel p = sub-panels [p PK, p PK + PK) (clamped to the last one: duplicates are never read)
   auto issue = [&](int p) {
-    bf16* s = smem + (p % R) * SLOT;
 #pragma unroll
-    for (int j = 0; j < DA; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + p * 64),
-                                       (__attribute__((address_space(3))) void*)(s + (wid * (ROWS / 4) + j * 8) * 64), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(srcW + p * 64),
-                                     (__attribute__((address_space(3))) void*)(s + (ROWS + wid * 8) * 64), 16, 0, 0);
+    for (int u = 0; u < PK; ++u) {
+      const int sp = min(p * PK + u, NS - 1);
+      bf16* s = smem + (p % R) * SLOT + u * SUB;
+#pragma unroll
+      for (int j = 0; j < DA; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + sp * 64),
+                                         (__attribute__((address_space(3))) void*)(s + (wid * (ROWS / 4) + j * 8) * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(srcW + sp * 64),
+                                       (__attribute__((address_space(3))) void*)(s + (ROWS + wid * 8) * 64), 16, 0, 0);
+    }
   };
 
   f32x4 acc[HALF];
@@ -230,21 +238,25 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   const int pre = min(R - 1, NP);
   for (int p = 0; p < pre; ++p) issue(p);
   for (int p = 0; p < NP; ++p) {
-    vm_wait(min(NP - 1 - p, R - 2) * DPP);            // this wave's DMAs of panel p have landed
-    asm volatile("s_barrier" ::: "memory");           // ... everyone's; slot of panel p-1 is free
+    vm_wait(min(NP - 1 - p, R - 2) * DPP);            // this wave's DMAs of super-panel p have landed
+    asm volatile("s_barrier" ::: "memory");           // ... everyone's; slot of super-panel p-1 is free
     __builtin_amdgcn_sched_barrier(0);
     if (p + R - 1 < NP) issue(p + R - 1);
-    const bf16* sA = smem + (p % R) * SLOT;
-    const bf16* sW = sA + ROWS * 64;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = kk * 4 + (lane >> 4);
-      const bf16x8 fb = *(const bf16x8*)(sW + dswz(wc * 16 + (lane & 15), ch));
-      bf16x8 fa[HALF];
+    for (int u = 0; u < PK; ++u) {
+      if (p * PK + u >= NS) break;
+      const bf16* sA = smem + (p % R) * SLOT + u * SUB;
+      const bf16* sW = sA + ROWS * 64;
 #pragma unroll
-      for (int i = 0; i < HALF; ++i) fa[i] = *(const bf16x8*)(sA + dswz((wr * HALF + i) * 16 + (lane & 15), ch));
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+        const bf16x8 fb = *(const bf16x8*)(sW + dswz(wc * 16 + (lane & 15), ch));
+        bf16x8 fa[HALF];
 #pragma unroll
-      for (int i = 0; i < HALF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[i], 0, 0, 0);
+        for (int i = 0; i < HALF; ++i) fa[i] = *(const bf16x8*)(sA + dswz((wr * HALF + i) * 16 + (lane & 15), ch));
+#pragma unroll
+        for (int i = 0; i < HALF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[i], 0, 0, 0);
+      }
     }
   }
 
@@ -262,14 +274,45 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   }
 }
 
+// Sub-panels of 64 k per ring slot: one barrier per PK x 64 of K, fewer slots to stay within 144 KiB.  Default
+// 4 where 3+ such slots fit (32/64-row blocks), else 2 (VLOG_AMD_RING_PK=1|2|4 overrides).  Measured on the
+// 150-row large-v3 decode: dec_gemm 405.6 (PK 1) / 391.2 (2) / 380.1 (4) ms per step, identical tokens.
+static int ring_pk() {
+  static const int v = [] {
+    const char* e = std::getenv("VLOG_AMD_RING_PK");
+    return e ? std::atoi(e) : 4;
+  }();
+  return v;
+}
+
 template <int MF, int KIND>
 static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      int splitk, int kr, hipStream_t st) {
   constexpr int R = MF <= 4 ? 8 : MF <= 8 ? 7 : 6;     // (MF*16 + 32) * 128 B per slot, <= 144 KiB in all
+  constexpr int SUBB = (MF * 16 + 32) * 128;           // bytes of one 64-k sub-panel
+  constexpr int R2 = std::min(8, (144 * 1024) / (2 * SUBB)), R4 = std::min(8, (144 * 1024) / (4 * SUBB));
   const int tiles_n = (N + 31) / 32;
   const int rgroups = (M + MF * 16 - 1) / (MF * 16);
-  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R>), dim3(tiles_n * rgroups * splitk), dim3(256), 0, st, a, w, ldw, M, N,
-                     K, epi, tiles_n, splitk, kr, ws, rgroups);
+  const dim3 grid(tiles_n * rgroups * splitk);
+  const int pk = ring_pk();
+  if constexpr (R4 >= 3) {
+    if (pk == 4) {
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R4, 4>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+                         splitk, kr, ws, rgroups);
+      WM_LAUNCH_CHECK("dec_ring_kernel");
+      return;
+    }
+  }
+  if constexpr (R2 >= 3) {
+    if (pk >= 2) {
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R2, 2>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+                         splitk, kr, ws, rgroups);
+      WM_LAUNCH_CHECK("dec_ring_kernel");
+      return;
+    }
+  }
+  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk, kr,
+                     ws, rgroups);
   WM_LAUNCH_CHECK("dec_ring_kernel");
 }
 

@@ -686,9 +686,11 @@ class BatchedInferencePipeline:
 
     def decode_windows(self, features: torch.Tensor, windows: Sequence[Tuple[int, int]], time_offsets: Sequence[float],
                        tokenizer: Tokenizer, options: TranscriptionOptions, seed: int = 0,
-                       files: Optional[Sequence[int]] = None) -> List[WindowResult]:
+                       files: Optional[Sequence[int]] = None,
+                       seek_bases: Optional[Sequence[int]] = None) -> List[WindowResult]:
         """files: the source file of each window when windows of several files share batches (transcribe_many):
-        word timestamps then keep one last-speech time per file."""
+        word timestamps then keep one last-speech time per file.  seek_bases: frame offset of each window's file
+        inside `features` (its segments and word timestamps are reported relative to the file)."""
         m = self.model
         eng = m.engine
         st = m.dims.specials
@@ -742,7 +744,8 @@ class BatchedInferencePipeline:
                 batch = []
                 for i, (s, n) in enumerate(wins):
                     r, alp, T, cr = results[i]
-                    wr = WindowResult(b0 + i, s, n, time_offsets[b0 + i], r.tokens, alp, T, cr, r.no_speech_prob)
+                    sb = seek_bases[b0 + i] if seek_bases is not None else 0
+                    wr = WindowResult(b0 + i, s - sb, n, time_offsets[b0 + i], r.tokens, alp, T, cr, r.no_speech_prob)
                     wr.segments = self.window_segments(wr, tokenizer, options)
                     batch.append(wr)
                 if options.word_timestamps:
@@ -843,13 +846,10 @@ class BatchedInferencePipeline:
                     offsets.append(s * HOP_LENGTH / SAMPLE_RATE)
                     fids.append(i)
                 base += preps[i]["features"].shape[1]
-            results = self.decode_windows(feats, windows, offsets, tokenizer, options, files=fids)
+            results = self.decode_windows(feats, windows, offsets, tokenizer, options, files=fids,
+                                          seek_bases=[bases[f] for f in fids])
             for i in files:
                 mine = [wr for wr, f in zip(results, fids) if f == i]
-                for wr in mine:                      # seeks relative to the file again
-                    wr.seek -= bases[i]
-                    for sg in wr.segments or []:
-                        sg["seek"] = wr.seek
                 out[i] = (list(self._segments(None, mine, tokenizer, options)), self._info(preps[i], options))
         return out
 
