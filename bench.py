@@ -55,8 +55,20 @@ def build_shard(rank: int, W: int):
 
 
 class Pipeline:
-    def __init__(self, eng, tok, dims, rank, world, W, beam, pcm_dev, margin_left, n_total, host_group=None):
+    def __init__(self, eng, tok, dims, rank, world, W, beam, pcm_dev, margin_left, n_total, host_group=None,
+                 words: bool = False):
         self.eng, self.tok, self.dims = eng, tok, dims
+        self.words = words
+        if words:
+            # the product's word-timestamp glue (WhisperModel.add_word_timestamps / find_alignment: one batched
+            # wm_align_batch over every window with text), bound to this engine
+            import functools
+            import types
+            from vlog_amd.transcribe import FRAMES_PER_SECOND, TOKENS_PER_SECOND, WhisperModel
+            m = types.SimpleNamespace(engine=eng, dims=dims, frames_per_second=FRAMES_PER_SECOND,
+                                      tokens_per_second=TOKENS_PER_SECOND)
+            m.find_alignment = functools.partial(WhisperModel.find_alignment, m)
+            self._add_words = functools.partial(WhisperModel.add_word_timestamps, m)
         self.host_group = host_group
         self.keep_windows = ()                  # windows whose encoder output the next step copies to the host
         self.rank, self.world, self.W, self.beam = rank, world, W, beam
@@ -89,10 +101,21 @@ class Pipeline:
         res, steps = eng.generate(list(range(W)), [self.prompt] * W, beam_size=self.beam, suppress_tokens=self.suppress,
                                   max_length=448, check_every=8)
         t3 = time.perf_counter()
-        segs = []
+        groups = []
         for w, r in enumerate(res):
             off = (self.rank * W + w) * 30.0
             cur, _, _ = split_segments_by_timestamps(r.tokens, d.specials.timestamp_begin, off, 3000, 30.0, w * 3000)
+            groups.append(cur)
+        t_al = 0.0
+        if self.words:
+            ta = time.perf_counter()
+            idx = [w for w, g in enumerate(groups) if g]
+            if idx:
+                self._add_words([groups[w] for w in idx], self.tok, [3000] * len(idx), "\"'“¿([{-",
+                                "\"'.。,，!！?？:：”)]}、", 0.0, slots=idx)
+            t_al = time.perf_counter() - ta
+        segs = []
+        for cur in groups:
             for s in cur:
                 text = self.tok.decode(s["tokens"])
                 if s["start"] == s["end"] or not text.strip():
@@ -100,7 +123,8 @@ class Pipeline:
                 segs.append({"start": s["start"], "end": s["end"], "text": text})
         vtt = generate_webvtt(segs)
         t4 = time.perf_counter()
-        for k, v in (("logmel", t1 - t0), ("encode", t2 - t1), ("decode", t3 - t2), ("host", t4 - t3)):
+        for k, v in (("logmel", t1 - t0), ("encode", t2 - t1), ("decode", t3 - t2), ("align", t_al),
+                     ("host", t4 - t3 - t_al)):
             self.stage[k] = self.stage.get(k, 0.0) + v
         import zlib
         crc = 0
@@ -242,6 +266,7 @@ def main():
     ap.add_argument("--model", default="large-v3")
     ap.add_argument("--windows", type=int, default=150, help="30 s windows per GPU")
     ap.add_argument("--beam", type=int, default=1)
+    ap.add_argument("--word-timestamps", action="store_true", help="config 5: batched word alignment in every step")
     ap.add_argument("--eot-after", type=int, default=110)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: profiles/traffic_r02_a.json, "
@@ -271,6 +296,8 @@ def main():
     eng = GpuEngine(dims, sd, local)
     if args.cross_fp8:
         eng.set_option("cross_fp8", 1)
+    if args.beam > 1 and not args.cross_fp8:
+        eng.set_option("cross_mode", 0)        # the product's choice for beam groups (transcribe.py decode_windows)
     keep_sd = rank == 0 and ((world == 1 and not args.no_cpu_baseline) or not args.no_parity)
     if not keep_sd:
         del sd
@@ -282,7 +309,8 @@ def main():
     n_total = world * W * CLIP
     eng.reserve(W, W * max(1, args.beam))
     log(f"[rank {rank}] setup {time.perf_counter() - t:.1f} s, engine {eng.device_bytes() / 2**30:.1f} GiB")
-    pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total, host_group)
+    pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total, host_group,
+                    words=args.word_timestamps)
 
     def barrier():
         torch.cuda.synchronize(eng.device)
@@ -348,8 +376,10 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16+e4m3-cross" if args.cross_fp8 else "bf16",
         "data": "synthetic",
         "config": {"workload": f"{args.model} bf16{' (opt-in fp8 e4m3 cross memory)' if args.cross_fp8 else ''} "
-                               f"{'greedy' if args.beam == 1 else 'beam%d' % args.beam}, timestamps on, "
-                               f"{W} x 30 s windows per GPU of the seeded speech-like corpus, window-sharded (config 4)",
+                               f"{'greedy' if args.beam == 1 else 'beam%d' % args.beam}, timestamps on"
+                               f"{', word timestamps' if args.word_timestamps else ''}, "
+                               f"{W} x 30 s windows per GPU of the seeded speech-like corpus, window-sharded "
+                               f"({'config 5' if args.beam > 1 and args.word_timestamps else 'config 4' if args.beam == 1 else 'beam search'})",
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
                    "token_crc32": pipe.last["crc"],
@@ -384,9 +414,13 @@ def main():
                 roof["traffic"] = tj.get(dom)
             except Exception:
                 pass
-        roof["accounting"] = ("factored cross-attention: algorithmic bytes = each active window's encoder output "
-                              + ("(L x 1500 x d e4m3 + 1500 f32 scales)" if args.cross_fp8 else "(L x 1500 x d bf16)")
-                              + " + q' per launch, counted in-kernel")
+        if args.beam > 1 and not args.cross_fp8:
+            roof["accounting"] = ("projected cross-attention (beam groups): algorithmic bytes = each active window's "
+                                  "K and V panels (L x 2 x 1500 x d bf16) per launch, counted in-kernel")
+        else:
+            roof["accounting"] = ("factored cross-attention: algorithmic bytes = each active window's encoder output "
+                                  + ("(L x 1500 x d e4m3 + 1500 f32 scales)" if args.cross_fp8 else "(L x 1500 x d bf16)")
+                                  + " + q' per launch, counted in-kernel")
         out["roofline"] = roof
         enc_ms = sum(breakdown[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
         enc_fl = sum(breakdown[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))

@@ -31,10 +31,12 @@ from vlog_amd.transcribe import WhisperModel  # noqa: E402
 from vlog_amd.vtt import generate_webvtt  # noqa: E402
 
 
-def worker_call(model, wav):
-    """The worker's TranscriptionWorker.transcribe + generate_webvtt (worker/transcription.py:92-133, 377)."""
+def worker_call(model, wav, temperature=None):
+    """The worker's TranscriptionWorker.transcribe + generate_webvtt (worker/transcription.py:92-133, 377).
+    temperature=None keeps faster-whisper's default fallback ladder (the worker's call as written)."""
     t = time.perf_counter()
-    segments, info = model.transcribe(str(wav), language=None, task="transcribe", beam_size=5, vad_filter=True)
+    kw = {} if temperature is None else {"temperature": temperature}
+    segments, info = model.transcribe(str(wav), language=None, task="transcribe", beam_size=5, vad_filter=True, **kw)
     segs, parts = [], []
     for s in segments:
         segs.append({"start": s.start, "end": s.end, "text": s.text})
@@ -48,6 +50,9 @@ def main():
     ap.add_argument("--model", default="large-v3")
     ap.add_argument("--minutes-seq", type=float, default=5.0)
     ap.add_argument("--minutes-tp", type=float, default=60.0)
+    ap.add_argument("--temperature", type=float, default=None,
+                    help="fixed temperature (e.g. 0: no fallback ladder, the cost of the call on a model whose windows "
+                         "pass faster-whisper's thresholds); default: the worker's call as written")
     args = ap.parse_args()
     model = WhisperModel(f"synthetic:{args.model}:0", device="cpu", compute_type="int8", eot_after=110)
     tmp = tempfile.mkdtemp()
@@ -62,18 +67,21 @@ def main():
     long_, long_s = clip(args.minutes_tp, "long.wav")
     out = {"model": args.model, "call": "transcribe(str(wav), language=None, task='transcribe', beam_size=5, "
                                         "vad_filter=True) + generate_webvtt"}
+    T = args.temperature
+    if T is not None:
+        out["temperature"] = T
     model.throughput = True
-    worker_call(model, short)                                      # warm-up (allocations, kernels)
+    worker_call(model, short, T)                                   # warm-up (allocations, kernels)
     model.throughput = False
-    dt, text_seq, info, nseg, _ = worker_call(model, short)
+    dt, text_seq, info, nseg, _ = worker_call(model, short, T)
     out["sequential"] = {"audio_s": short_s, "wall_s": round(dt, 3), "rtfx": round(short_s / dt, 2), "segments": nseg,
                          "duration_after_vad": round(info.duration_after_vad, 2)}
     model.throughput = True
-    dt, text_tp, info, nseg, _ = worker_call(model, short)
+    dt, text_tp, info, nseg, _ = worker_call(model, short, T)
     out["throughput_same_clip"] = {"audio_s": short_s, "wall_s": round(dt, 3), "rtfx": round(short_s / dt, 2),
                                    "segments": nseg}
     out["wer_throughput_vs_sequential"] = round(word_error_rate(text_seq, text_tp), 4)
-    dt, _, info, nseg, _ = worker_call(model, long_)
+    dt, _, info, nseg, _ = worker_call(model, long_, T)
     out["throughput"] = {"audio_s": long_s, "wall_s": round(dt, 3), "rtfx": round(long_s / dt, 2), "segments": nseg,
                          "duration_after_vad": round(info.duration_after_vad, 2)}
     print(json.dumps(out), flush=True)

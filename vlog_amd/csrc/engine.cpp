@@ -1151,6 +1151,19 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
       const int p = std::atoi(v) != 0;
       for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[p][i];
     }
+    if (const char* v = std::getenv("VLOG_AMD_DEC_GEMM")) {       // per projection, e.g. "qkv=32,fc2=64"
+      std::string spec(v);
+      size_t pos = 0;
+      while (pos < spec.size()) {
+        const size_t end = std::min(spec.find(',', pos), spec.size());
+        const std::string item = spec.substr(pos, end - pos);
+        const size_t eq = item.find('=');
+        if (eq != std::string::npos)
+          for (int i = 0; i < DEC_NPROJ; ++i)
+            if (item.substr(0, eq) == kDecProjNames[i]) e->dec_plan[i] = std::atoi(item.c_str() + eq + 1);
+        pos = end + 1;
+      }
+    }
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));

@@ -704,9 +704,16 @@ class BatchedInferencePipeline:
         out: List[WindowResult] = []
         B = self.max_batch_windows
         per = max(options.beam_size, options.best_of, 1)
+        # cross-attention form per batch: the factored form (attention over the encoder output) reads half the
+        # bytes per window and wins for one row per window; with beam / best-of groups the projected K/V form
+        # wins (large-v3, 150 windows, beam 5 + words: 1474 vs 1237 RTFx) because every group's rows share one
+        # K/V stream there, while the factored kernel re-reads E per 32 (row, head) pairs
+        auto_form = os.environ.get("VLOG_AMD_CROSS_AUTO", "1") != "0"
         for b0 in range(0, len(windows), B):
             wins = list(windows[b0: b0 + B])
             with m._lock:
+                if auto_form:
+                    eng.set_option("cross_mode", 0 if per > 1 else 1)
                 eng.reserve(len(wins), len(wins) * per)
                 enc = eng.encode(features, [w[0] for w in wins], [w[1] for w in wins])
                 eng.cross_kv(enc, 0)
