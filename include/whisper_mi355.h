@@ -40,6 +40,10 @@ int32_t wm_abi_version(void);
 int wm_set_weight(wm_engine* e, const char* name, const void* d_src, int64_t nbytes, void* stream);
 /* 1 when every weight has been set. */
 int32_t wm_weights_complete(wm_engine* e);
+/* The weights wm_set_weight expects, in layout order (for bindings that do not carry this table, e.g. a C or
+ * Go host): name (owned by the engine), size in bytes, element bytes (2 = bf16 matrix, 4 = f32). */
+int32_t wm_weight_count(wm_engine* e);
+int wm_weight_info(wm_engine* e, int32_t i, const char** name, int64_t* nbytes, int32_t* elem_bytes);
 
 /* Log-mel, replacing faster-whisper FeatureExtractor.__call__ [FW↑] (reached from
  * worker/transcription.py:105).  Computes frames [frame0, frame0+n_frames) of the WHOLE-FILE spectrogram

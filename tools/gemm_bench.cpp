@@ -55,6 +55,9 @@ int main(int argc, char** argv) {
       {"dec.fc1  (150 rows)", 150, 5120, 1280, EPI_BF16},
       {"dec.fc2  (150 rows)", 150, 1280, 5120, EPI_RESID_F32},
       {"dec.out  (150 rows)", 150, 1280, 1280, EPI_RESID_F32},
+      {"square 4096", 4096, 4096, 4096, EPI_BF16},             // the guide's 8-phase template reference shape
+      {"square 8192", 8192, 8192, 8192, EPI_BF16},
+      {"enc.qkv K=4096", 24000, 3840, 4096, EPI_BF16},         // same tiles, 3.2x the K loop
   };
   size_t maxA = 0, maxW = 0, maxC = 0;
   for (auto& s : shapes) {

@@ -15,7 +15,7 @@ ABI_VERSION = 1
 
 # Every entry point include/whisper_mi355.h declares (tests check the library exports all of them).
 SYMBOLS = (
-    "wm_create", "wm_destroy", "wm_last_error", "wm_abi_version", "wm_set_weight", "wm_weights_complete",
+    "wm_create", "wm_destroy", "wm_last_error", "wm_abi_version", "wm_set_weight", "wm_weights_complete", "wm_weight_count", "wm_weight_info",
     "wm_logmel", "wm_logmel_finalize", "wm_encode", "wm_reserve", "wm_cross_kv", "wm_generate", "wm_forward",
     "wm_frame_energy", "wm_pcm_from_s16", "wm_vad_probs", "wm_cross_fp8_quantize", "wm_align", "wm_align_batch", "wm_dtw", "wm_device_bytes", "wm_profile_classes", "wm_profile_name", "wm_profile", "wm_profile_select",
     "wm_profile_read", "wm_set_option", "wm_encoder_attention",
@@ -61,6 +61,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "wm_abi_version": (i32, []),
         "wm_set_weight": (C.c_int, [vp, C.c_char_p, vp, i64, vp]),
         "wm_weights_complete": (i32, [vp]),
+        "wm_weight_count": (i32, [vp]),
+        "wm_weight_info": (C.c_int, [vp, i32, C.POINTER(C.c_char_p), C.POINTER(i64), C.POINTER(i32)]),
         "wm_logmel": (C.c_int, [vp, vp, i64, i64, i64, i32, vp, i64, vp, vp]),
         "wm_logmel_finalize": (C.c_int, [vp, vp, i64, i64, vp, C.POINTER(C.c_float), C.POINTER(C.c_float), vp]),
         "wm_encode": (C.c_int, [vp, vp, i64, C.POINTER(i32), C.POINTER(i32), i32, vp, vp]),

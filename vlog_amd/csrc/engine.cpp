@@ -98,6 +98,7 @@ struct DevBuf {
 struct Slot {
   size_t off, bytes;
   bool set = false;
+  int elem = 2;              // element bytes: 2 = bf16 matrix, 4 = f32 vector / table
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -121,6 +122,7 @@ struct wm_engine {
   std::mutex mu;
   // weights
   std::map<std::string, Slot> slots;
+  std::vector<std::string> slot_order;   // weight names in layout order (wm_weight_info)
   DevBuf arena;
   int k1p;  // padded conv1 K
   // frontend constants
@@ -209,9 +211,10 @@ struct wm_engine {
 
 namespace {
 
-void add_slot(wm_engine* e, size_t& off, const std::string& name, size_t bytes) {
-  e->slots[name] = Slot{off, bytes, false};
-  off += align256(bytes);
+void add_slot(wm_engine* e, size_t& off, const std::string& name, size_t count, int elem) {
+  e->slots[name] = Slot{off, count * elem, false, elem};
+  e->slot_order.push_back(name);
+  off += align256(count * elem);
 }
 
 void build_layout(wm_engine* e) {
@@ -219,38 +222,38 @@ void build_layout(wm_engine* e) {
   const size_t d = m.n_state, f = 4 * d, b2 = 2, f4 = 4;
   e->k1p = ((3 * m.n_mels + 63) / 64) * 64;
   size_t off = 0;
-  add_slot(e, off, "enc.conv1.w", d * e->k1p * b2);
-  add_slot(e, off, "enc.conv1.b", d * f4);
-  add_slot(e, off, "enc.conv2.w", d * 3 * d * b2);
-  add_slot(e, off, "enc.conv2.b", d * f4);
-  add_slot(e, off, "enc.pos", (size_t)m.n_audio_ctx * d * f4);
+  add_slot(e, off, "enc.conv1.w", d * e->k1p, 2);
+  add_slot(e, off, "enc.conv1.b", d, 4);
+  add_slot(e, off, "enc.conv2.w", d * 3 * d, 2);
+  add_slot(e, off, "enc.conv2.b", d, 4);
+  add_slot(e, off, "enc.pos", (size_t)m.n_audio_ctx * d, 4);
   for (int l = 0; l < m.n_enc_layer; ++l) {
     const std::string p = "enc." + std::to_string(l) + ".";
-    add_slot(e, off, p + "ln1.w", d * f4); add_slot(e, off, p + "ln1.b", d * f4);
-    add_slot(e, off, p + "qkv.w", 3 * d * d * b2); add_slot(e, off, p + "qkv.b", 3 * d * f4);
-    add_slot(e, off, p + "out.w", d * d * b2); add_slot(e, off, p + "out.b", d * f4);
-    add_slot(e, off, p + "ln2.w", d * f4); add_slot(e, off, p + "ln2.b", d * f4);
-    add_slot(e, off, p + "fc1.w", f * d * b2); add_slot(e, off, p + "fc1.b", f * f4);
-    add_slot(e, off, p + "fc2.w", d * f * b2); add_slot(e, off, p + "fc2.b", d * f4);
+    add_slot(e, off, p + "ln1.w", d, 4); add_slot(e, off, p + "ln1.b", d, 4);
+    add_slot(e, off, p + "qkv.w", 3 * d * d, 2); add_slot(e, off, p + "qkv.b", 3 * d, 4);
+    add_slot(e, off, p + "out.w", d * d, 2); add_slot(e, off, p + "out.b", d, 4);
+    add_slot(e, off, p + "ln2.w", d, 4); add_slot(e, off, p + "ln2.b", d, 4);
+    add_slot(e, off, p + "fc1.w", f * d, 2); add_slot(e, off, p + "fc1.b", f, 4);
+    add_slot(e, off, p + "fc2.w", d * f, 2); add_slot(e, off, p + "fc2.b", d, 4);
   }
-  add_slot(e, off, "enc.ln.w", d * f4); add_slot(e, off, "enc.ln.b", d * f4);
-  add_slot(e, off, "dec.embed", (size_t)m.n_vocab * d * b2);
-  add_slot(e, off, "dec.pos", (size_t)m.n_text_ctx * d * f4);
+  add_slot(e, off, "enc.ln.w", d, 4); add_slot(e, off, "enc.ln.b", d, 4);
+  add_slot(e, off, "dec.embed", (size_t)m.n_vocab * d, 2);
+  add_slot(e, off, "dec.pos", (size_t)m.n_text_ctx * d, 4);
   for (int l = 0; l < m.n_dec_layer; ++l) {
     const std::string p = "dec." + std::to_string(l) + ".";
-    add_slot(e, off, p + "ln1.w", d * f4); add_slot(e, off, p + "ln1.b", d * f4);
-    add_slot(e, off, p + "qkv.w", 3 * d * d * b2); add_slot(e, off, p + "qkv.b", 3 * d * f4);
-    add_slot(e, off, p + "out.w", d * d * b2); add_slot(e, off, p + "out.b", d * f4);
-    add_slot(e, off, p + "ln2.w", d * f4); add_slot(e, off, p + "ln2.b", d * f4);
-    add_slot(e, off, p + "cq.w", d * d * b2); add_slot(e, off, p + "cq.b", d * f4);
-    add_slot(e, off, p + "cout.w", d * d * b2); add_slot(e, off, p + "cout.b", d * f4);
-    add_slot(e, off, p + "ln3.w", d * f4); add_slot(e, off, p + "ln3.b", d * f4);
-    add_slot(e, off, p + "fc1.w", f * d * b2); add_slot(e, off, p + "fc1.b", f * f4);
-    add_slot(e, off, p + "fc2.w", d * f * b2); add_slot(e, off, p + "fc2.b", d * f4);
+    add_slot(e, off, p + "ln1.w", d, 4); add_slot(e, off, p + "ln1.b", d, 4);
+    add_slot(e, off, p + "qkv.w", 3 * d * d, 2); add_slot(e, off, p + "qkv.b", 3 * d, 4);
+    add_slot(e, off, p + "out.w", d * d, 2); add_slot(e, off, p + "out.b", d, 4);
+    add_slot(e, off, p + "ln2.w", d, 4); add_slot(e, off, p + "ln2.b", d, 4);
+    add_slot(e, off, p + "cq.w", d * d, 2); add_slot(e, off, p + "cq.b", d, 4);
+    add_slot(e, off, p + "cout.w", d * d, 2); add_slot(e, off, p + "cout.b", d, 4);
+    add_slot(e, off, p + "ln3.w", d, 4); add_slot(e, off, p + "ln3.b", d, 4);
+    add_slot(e, off, p + "fc1.w", f * d, 2); add_slot(e, off, p + "fc1.b", f, 4);
+    add_slot(e, off, p + "fc2.w", d * f, 2); add_slot(e, off, p + "fc2.b", d, 4);
   }
-  add_slot(e, off, "dec.ckv.w", (size_t)m.n_dec_layer * 2 * d * d * b2);
-  add_slot(e, off, "dec.ckv.b", (size_t)m.n_dec_layer * 2 * d * f4);
-  add_slot(e, off, "dec.ln.w", d * f4); add_slot(e, off, "dec.ln.b", d * f4);
+  add_slot(e, off, "dec.ckv.w", (size_t)m.n_dec_layer * 2 * d * d, 2);
+  add_slot(e, off, "dec.ckv.b", (size_t)m.n_dec_layer * 2 * d, 4);
+  add_slot(e, off, "dec.ln.w", d, 4); add_slot(e, off, "dec.ln.b", d, 4);
   e->arena.ensure(off);
 }
 
@@ -1138,6 +1141,12 @@ int32_t wm_abi_version(void) { return 1; }
 int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
   try {
     if (!dims || !out) throw std::runtime_error("wm_create: null argument");
+    *out = nullptr;
+    if (dims->n_head <= 0 || dims->n_state <= 0 || dims->n_mels <= 0 || dims->n_enc_layer <= 0 ||
+        dims->n_dec_layer <= 0 || dims->n_vocab <= 0 || dims->n_text_ctx <= 0 || dims->n_text_ctx > 448)
+      throw std::runtime_error("wm_create: dimensions must be positive (n_text_ctx <= 448)");
+    for (int32_t t : {dims->eot, dims->sot, dims->no_speech, dims->no_timestamps, dims->timestamp_begin, dims->blank})
+      if (t < 0 || t >= dims->n_vocab) throw std::runtime_error("wm_create: special token id out of the vocabulary");
     if (dims->n_state % 64 != 0 || dims->n_state / dims->n_head != 64)
       throw std::runtime_error("wm_create: head_dim must be 64 and n_state a multiple of 64");
     if (dims->n_audio_ctx != 1500) throw std::runtime_error("wm_create: n_audio_ctx must be 1500");
@@ -1215,6 +1224,19 @@ int wm_set_weight(wm_engine* e, const char* name, const void* d_src, int64_t nby
     HIP_OK(hipMemcpyAsync((char*)e->arena.p + it->second.off, d_src, nbytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     it->second.set = true;
     if (it->first == "dec.ckv.w") e->xwkt_ready = false;
+  });
+}
+
+int32_t wm_weight_count(wm_engine* e) { return e ? (int32_t)e->slot_order.size() : 0; }
+
+int wm_weight_info(wm_engine* e, int32_t i, const char** name, int64_t* nbytes, int32_t* elem_bytes) {
+  return guarded(e, [&] {
+    if (i < 0 || i >= (int32_t)e->slot_order.size()) throw std::runtime_error("wm_weight_info: index out of range");
+    const auto& nm = e->slot_order[i];
+    const Slot& s = e->slots.at(nm);
+    if (name) *name = nm.c_str();
+    if (nbytes) *nbytes = (int64_t)s.bytes;
+    if (elem_bytes) *elem_bytes = s.elem;
   });
 }
 
