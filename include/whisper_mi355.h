@@ -49,8 +49,9 @@ int wm_weight_info(wm_engine* e, int32_t i, const char** name, int64_t* nbytes, 
  * worker/transcription.py:105).  Computes frames [frame0, frame0+n_frames) of the WHOLE-FILE spectrogram
  * (file of n_samples samples; d_pcm[i] is file sample pcm_offset+i) as log10(max(mel, 1e-10)) into
  * d_mel[m*ld + f], and folds their maximum into *d_gmax (order-preserving uint32, zero-initialised by the
- * caller).  wm_logmel_finalize applies max(x, gmax-8), (x+4)/4 in place; gmax is taken from h_gmax when
- * non-NULL (cross-shard max), else from d_gmax. */
+ * caller).  frame0 must be even: frames are transformed in (even, odd) pairs, so any split of a file into
+ * even-aligned frame ranges gives bit-identical frames.  wm_logmel_finalize applies max(x, gmax-8), (x+4)/4
+ * in place; gmax is taken from h_gmax when non-NULL (cross-shard max), else from d_gmax. */
 int wm_logmel(wm_engine* e, const float* d_pcm, int64_t pcm_offset, int64_t n_samples, int64_t frame0,
               int32_t n_frames, float* d_mel, int64_t ld, uint32_t* d_gmax, void* stream);
 int wm_logmel_finalize(wm_engine* e, float* d_mel, int64_t n_frames, int64_t ld, const uint32_t* d_gmax,

@@ -1250,6 +1250,7 @@ int32_t wm_weights_complete(wm_engine* e) {
 int wm_logmel(wm_engine* e, const float* d_pcm, int64_t pcm_offset, int64_t n_samples, int64_t frame0, int32_t n_frames,
               float* d_mel, int64_t ld, uint32_t* d_gmax, void* stream) {
   return guarded(e, [&] {
+    if (frame0 % 2) throw std::runtime_error("wm_logmel: frame0 must be even (frames are transformed in pairs)");
     const long long n_padded = n_samples + 160;
     ProfScope ps(e, P_LOGMEL, (hipStream_t)stream, 2.0 * 201 * 400 * 2 * n_frames, 4.0 * 160 * n_frames + 4.0 * e->dm.n_mels * n_frames);
     launch_logmel(d_pcm, pcm_offset, n_samples, n_padded, frame0, n_frames, e->fe_window.as<float>(), e->fe_cos.as<float>(),

@@ -104,8 +104,10 @@ class StreamingIngest:
         if final:
             ready = (self.n + HOP_LENGTH) // HOP_LENGTH          # N // 160 + 1 frames in all
         else:
-            # frame f reads samples [160 f - 200, 160 f + 200): complete once 160 f + 200 <= n
+            # frame f reads samples [160 f - 200, 160 f + 200): complete once 160 f + 200 <= n; frames are
+            # transformed in (even, odd) pairs, so a chunk ends on an even frame (bit-identical to one shot)
             ready = max(0, (self.n - N_FFT // 2) // HOP_LENGTH + 1) if self.n >= N_FFT // 2 else 0
+            ready &= ~1
         if ready <= self.done:
             return
         nf = ready - self.done

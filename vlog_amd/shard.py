@@ -61,7 +61,7 @@ def plan_shards(n_samples: int, world: int) -> List[ShardPlan]:
     n_win = max(1, -(-cf // N_FRAMES))
     plans = []
     for rank, (w0, w1) in enumerate(partition_windows(n_win, world)):
-        f0 = min(w0 * N_FRAMES, cf + 1)
+        f0 = min(w0 * N_FRAMES, (cf + 1) & ~1)   # even: the log-mel kernel transforms (even, odd) frame pairs
         f1 = min(cf, w1 * N_FRAMES)
         if w1 == n_win and w1 > w0:
             f1 = cf + 1                      # the shard with the last window also owns the trailing frame
