@@ -190,8 +190,7 @@ struct XAttnArgs {
   int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0): bit 0 skips
                                          // the S MFMAs, bit 1 the cross-wave sum, bit 2 the U phase, bit 3
                                          // loads E with plain loads (same-box bench: 1 % slower than
-                                         // non-temporal ones; tools/gpu_ablib.sh), bit 4 skips the E loads,
-                                         // bit 5 the LDS image writes
+                                         // non-temporal ones; tools/gpu_ablib.sh), bit 4 skips the E loads
 };
 
 // One work item: rows of group `grp` x (row, head) m-tile `mt`, key tiles [tb, te) written as partial `split`.
@@ -279,7 +278,6 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     int r = lo / CPR, ch = lo % CPR;     // chunk (r, ch) of load i, stepped like the global offsets
 #pragma unroll
     for (int i = 0; i < LS; ++i) {
-      if (a.abl & 32) break;             // ablation: no LDS image writes
       if (i) {
         ch += 64 % CPR;
         r += 64 / CPR;
