@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   for (int f8 = 0; f8 < 2; ++f8) {
     const double bytes = (double)W * T * d * (f8 ? 1 : 2);
-    for (int abl : {0, 1, 2, 4, 7, 16, 23, 55, 32}) {
+    for (int abl : {0, 1, 2, 4, 7, 16, 23}) {
       xattn_set_ablation(abl);
       for (int splits : split_list) {
         auto run = [&] {

@@ -187,14 +187,15 @@ struct XAttnArgs {
   float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
   float* probs; const int* head_map; int n_align;   // capture: raw scores [row][n_align][T]
   unsigned long long* stat;
-  int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0): bit 0 skips
+  int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0, and the
+                                         // product kernel is compiled without them: template ABL): bit 0 skips
                                          // the S MFMAs, bit 1 the cross-wave sum, bit 2 the U phase, bit 3
                                          // loads E with plain loads (same-box bench: 1 % slower than
                                          // non-temporal ones; tools/gpu_ablib.sh), bit 4 skips the E loads
 };
 
 // One work item: rows of group `grp` x (row, head) m-tile `mt`, key tiles [tb, te) written as partial `split`.
-template <int QW, int NW, int DEPTH, bool F8>
+template <int QW, int NW, int DEPTH, bool F8, int ABL, bool CAP>
 __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, int grp, int mt, int split, int tb,
                                               int te) {
   constexpr int KS = QW / 16, CT = QW / 32, LDR = xldr(QW), CPR = F8 ? QW / 16 : QW / 8, LS = F8 ? KS / 2 : KS;
@@ -245,7 +246,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   i32x4 stgA[LS], stgB[LS];
   float scA = 1.f, scB = 1.f;            // F8: lane l (< 32) stages the scale of position tile*32 + l
   auto load = [&](i32x4 (&stg)[LS], float& scl, int tile, int lo) {
-    if (a.abl & 16) {                    // ablation: no E loads (compute-only timing)
+    if (ABL & 16) {                    // ablation: no E loads (compute-only timing)
 #pragma unroll
       for (int i = 0; i < LS; ++i) stg[i] = i32x4{0x3c003c00 + lo, 0x3c003c00, 0x3c003c00, 0x3c003c00 + tile};
       scl = 1.f;
@@ -256,7 +257,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
       const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
       const int t = min(tile * 32 + r, a.T - 1);
       const i32x4* src = (const i32x4*)(E + ((long long)t * a.d) * EB + ch * 16);
-      if (a.abl & 8) stg[i] = *src;
+      if (ABL & 8) stg[i] = *src;
       else stg[i] = __builtin_nontemporal_load(src);
     }
     if (F8) scl = Es[min(tile * 32 + (lo & 31), a.T - 1)];
@@ -310,7 +311,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
       const int l32o = lo & 31, g = (l32o >> 2) & 3;
       const bf16* s0 = sE + l32o * LDR + 8 * (hh ^ g);
       const bf16* s1 = sE + l32o * LDR + 8 * ((2 + hh) ^ g);
-      if (!(a.abl & 1)) {
+      if (!(ABL & 1)) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           const bf16x8 ea = *(const bf16x8*)(((s & 1) ? s1 : s0) + 32 * (s >> 1));
@@ -320,7 +321,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     }
     // the NW partials -> the full S^T in every wave: partials to LDS; wave w sums registers
     // [w RPW, (w+1) RPW) over the waves in a fixed order (0..NW-1); every wave reads the 16 sums back
-    if (!(a.abl & 2)) {
+    if (!(ABL & 2)) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sX[(wv * 16 + r) * 64 + lane] = sc[r];
       __syncthreads();
@@ -356,7 +357,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
       for (int r = 0; r < 16; ++r)
         if (t0 + 8 * (r >> 2) + 4 * hh + (r & 3) >= a.T) sc[r] = -INFINITY;
     }
-    if (pr_row) {
+    if (CAP && pr_row) {                 // alignment capture: a separate instantiation (CAP)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int t = t0 + 8 * (r >> 2) + 4 * hh + (r & 3);
@@ -388,7 +389,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     // ---- U^T (wave cols) += E^T . P^T.  Transposed read of rows 16 ks + 8 jh + 4 hh + gq, columns
     // 32 c + 16 (G4 & 1) + 4 gp: chunk 4 c + lowc (lowc = 2 (G4 & 1) + (gp >> 1)) is stored at
     // 4 c + (lowc ^ (2 jh + hh)), so each jh has one base address and (ks, c) are immediate offsets.
-    if (!(a.abl & 4)) {
+    if (!(ABL & 4)) {
       const int G4 = (lo >> 4) & 3, gi = lo & 15, gq = gi >> 2, gp = gi & 3;
       const int lowc = 2 * (G4 & 1) + (gp >> 1);
       const bf16* tb0 = sE + (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
@@ -438,7 +439,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   }
 }
 
-template <int QW, int NW, int DEPTH, bool F8 = false>
+template <int QW, int NW, int DEPTH, bool F8 = false, int ABL = 0, bool CAP = false>
 __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   constexpr int LDR = xldr(QW);
   __shared__ __attribute__((aligned(16))) char smem[NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4 + (F8 ? NW * 32 * 4 : 0)];
@@ -450,7 +451,8 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   const int mt = item % a.n_mt;
   const int rest = item / a.n_mt;
   const int split = rest % a.splits, grp = rest / a.splits;
-  xattn_segment<QW, NW, DEPTH, F8>(a, smem, grp, mt, split, split * n_tiles / a.splits, (split + 1) * n_tiles / a.splits);
+  xattn_segment<QW, NW, DEPTH, F8, ABL, CAP>(a, smem, grp, mt, split, split * n_tiles / a.splits,
+                                        (split + 1) * n_tiles / a.splits);
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -695,10 +697,27 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
     const char* e = std::getenv("VLOG_AMD_XFORM");
     return e ? std::atoi(e) : 0;
   }();
+#define XA_LAUNCH_C(QW_, NW_, DP_, F8_, CAP_)                                                                      \
+  if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_, 0, CAP_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a); \
+  else hipLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_, 0, CAP_>), grid, dim3(NW_ * 64), 0, st, a);
 #define XA_LAUNCH_F(QW_, NW_, DP_, F8_)                                                                            \
-  if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a);   \
-  else hipLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_>), grid, dim3(NW_ * 64), 0, st, a);
+  if (probs) { XA_LAUNCH_C(QW_, NW_, DP_, F8_, true) } else { XA_LAUNCH_C(QW_, NW_, DP_, F8_, false) }
 #define XA_LAUNCH(QW_, NW_, DP_) XA_LAUNCH_F(QW_, NW_, DP_, false)
+  if (a.abl) {                           // microbenchmark ablations (tools/xattn_bench): d = 1280, default form only
+    if (d != 1280) throw std::runtime_error("xattn: ablations are built for n_state 1280 only");
+#define XA_ABL(F8_, AB_) \
+    case AB_: hipLaunchKernelGGL((xattn_kernel<160, 8, 1, F8_, AB_>), grid, dim3(512), 0, st, a); break;
+    if (escale) {
+      switch (a.abl) { XA_ABL(true, 1) XA_ABL(true, 2) XA_ABL(true, 4) XA_ABL(true, 7) XA_ABL(true, 8) XA_ABL(true, 16)
+                       XA_ABL(true, 23) default: throw std::runtime_error("xattn: unsupported ablation"); }
+    } else {
+      switch (a.abl) { XA_ABL(false, 1) XA_ABL(false, 2) XA_ABL(false, 4) XA_ABL(false, 7) XA_ABL(false, 8)
+                       XA_ABL(false, 16) XA_ABL(false, 23) default: throw std::runtime_error("xattn: unsupported ablation"); }
+    }
+#undef XA_ABL
+    WM_LAUNCH_CHECK("xattn_kernel");
+    return;
+  }
   if (escale) {                          // fp8 cross memory: the default forms only
     switch (d) {
       case 384: XA_LAUNCH_F(96, 4, 1, true); break;
@@ -728,6 +747,7 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
   }
 #undef XA_LAUNCH
 #undef XA_LAUNCH_F
+#undef XA_LAUNCH_C
   WM_LAUNCH_CHECK("xattn_kernel");
 }
 

@@ -242,9 +242,7 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
     asm volatile("s_barrier" ::: "memory");           // ... everyone's; slot of super-panel p-1 is free
     __builtin_amdgcn_sched_barrier(0);
     if (p + R - 1 < NP) issue(p + R - 1);
-#pragma unroll
-    for (int u = 0; u < PK; ++u) {
-      if (p * PK + u >= NS) break;
+    auto sub = [&](int u) {
       const bf16* sA = smem + (p % R) * SLOT + u * SUB;
       const bf16* sW = sA + ROWS * 64;
 #pragma unroll
@@ -257,6 +255,12 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
 #pragma unroll
         for (int i = 0; i < HALF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[i], 0, 0, 0);
       }
+    };
+    if (p * PK + PK <= NS) {              // a whole super-panel: no per-sub-panel branch in the MFMA stream
+#pragma unroll
+      for (int u = 0; u < PK; ++u) sub(u);
+    } else {
+      for (int u = 0; u < NS - p * PK; ++u) sub(u);
     }
   }
 
