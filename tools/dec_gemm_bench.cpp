@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
   const int krs[] = {128, 192, 256, 320, 448};
   size_t maxW = 0;
   for (auto& s : shapes) maxW = std::max(maxW, (size_t)s.N * s.K);
-  const size_t maxA = (size_t)M * 5120, maxC = (size_t)M * 5120;
+  const size_t maxA = (size_t)M * (5120 + 64), maxC = (size_t)M * 5120;
   std::mt19937 rng(1);
   std::uniform_real_distribution<float> U(-1.f, 1.f);
   std::vector<uint16_t> hA(maxA), hW(maxW);
@@ -149,21 +149,26 @@ int main(int argc, char** argv) {
       });
       std::printf("%s N=%5d K=%5d  launch_gemm        %7.2f us  %7.1f GB/s(W)\n", s.name, s.N, s.K, us, wbytes / us / 1e3);
     }
-    for (int rpb : {0, 32, 64, 96}) {
-      for (int kr : {0, 640, 1280, 2560, 5120}) {
-        if (kr > s.K || (kr > 0 && kr != s.K && s.K <= 1280)) continue;
-        CK(hipMemsetAsync(dC, 0, cbytes, st));
-        if (!launch_dec_ring(a, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb)) {
-          std::printf("ring kr=%d rows=%d unsupported\n", kr, rpb);
-          continue;
+    for (int pad : {0, 64}) {
+      // pad: activation row stride K + pad (a 64-element pad moves consecutive rows to different L2 channels)
+      const GemmA ap{dA, (long long)s.K + pad, 0, 0};
+      for (int rpb : {0, 32, 64, 96}) {
+        for (int kr : {0, 640, 1280, 2560, 5120}) {
+          if (kr > s.K || (kr > 0 && kr != s.K && s.K <= 1280)) continue;
+          if (pad && kr != 0) continue;
+          CK(hipMemsetAsync(dC, 0, cbytes, st));
+          if (!launch_dec_ring(ap, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb)) {
+            std::printf("ring kr=%d rows=%d unsupported\n", kr, rpb);
+            continue;
+          }
+          CK(hipStreamSynchronize(st));
+          const double err = f32 || pad ? 0.0 : maxdiff();
+          const double us = timeit([&](int r) {
+            launch_dec_ring(ap, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb);
+          });
+          std::printf("%s N=%5d K=%5d  RING kr=%4d rows=%3d pad=%2d %7.2f us  %7.1f GB/s(W)  rel diff %.1e\n", s.name, s.N,
+                      s.K, kr, rpb, pad, us, wbytes / us / 1e3, err);
         }
-        CK(hipStreamSynchronize(st));
-        const double err = f32 ? 0.0 : maxdiff();
-        const double us = timeit([&](int r) {
-          launch_dec_ring(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb);
-        });
-        std::printf("%s N=%5d K=%5d  RING kr=%4d rows=%3d %7.2f us  %7.1f GB/s(W)  rel diff %.1e\n", s.name, s.N, s.K, kr,
-                    rpb, us, wbytes / us / 1e3, err);
       }
     }
     for (int nc : {2, 4}) {

@@ -40,9 +40,22 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  // XB_ABL="0,7" restricts the ablation list, XB_F8=0|1 the cross-memory form (default: all).  Sustained
+  // runs lower the clock: the first configuration measured reads fastest, so compare in alternating order.
+  std::vector<int> abls = {0, 1, 2, 4, 7, 16, 23};
+  if (const char* e = getenv("XB_ABL")) {
+    abls.clear();
+    for (const char* p = e; *p;) {
+      abls.push_back(atoi(p));
+      while (*p && *p != ',') ++p;
+      if (*p) ++p;
+    }
+  }
+  const int f8_only = getenv("XB_F8") ? atoi(getenv("XB_F8")) : -1;
   for (int f8 = 0; f8 < 2; ++f8) {
+    if (f8_only >= 0 && f8 != f8_only) continue;
     const double bytes = (double)W * T * d * (f8 ? 1 : 2);
-    for (int abl : {0, 1, 2, 4, 7, 16, 23}) {
+    for (int abl : abls) {
       xattn_set_ablation(abl);
       for (int splits : split_list) {
         auto run = [&] {
