@@ -205,6 +205,10 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   per-projection fastest at 150 rows (tools/dec_gemm_bench).  "decode_gemm.<proj>" sets one projection:
  *   > 0 ring GEMM with the rows in groups of that many, 0 all-rows ring, -1 skinny split-K, -2 one-shot GEMM.
  *   Routes differ in K summation order (results agree to f32 rounding, not bit for bit).
+ *   "decode_gemm_cols.<proj>" (default 32): output columns per ring-GEMM block, 32 or 64 (64 takes row groups
+ *   of at most 64; other routes ignore it).  Bit-identical either way.
+ *   "cross_attn_snake" (default 0): odd decoder layers walk the factored cross-attention's items in reverse, so
+ *   the encoder output read last by one layer is read first by the next (Infinity Cache reuse).  Bit-identical.
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its
  *   (window, head, key split) items with a grid stride; 0 launches one block per item.
  *   "cross_attn_fuse" (default 1): bit 0 folds the cq projection's split-K combine into the cross-attention

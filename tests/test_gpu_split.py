@@ -41,6 +41,10 @@ def _run(eng, dims, split, opts=(), **kw):
     eng.set_option("decode_split", 0)                 # back to the defaults
     eng.set_option("cross_attn_fuse", 1)
     eng.set_option("cross_attn_blocks", 0)
+    eng.set_option("cross_attn_snake", 0)
+    eng.set_option("decode_gemm_plan", 1)
+    for pj in ("qkv", "out", "cq", "cout", "fc1", "fc2"):
+        eng.set_option("decode_gemm_cols." + pj, 32)
     return res, steps
 
 
@@ -61,6 +65,19 @@ def test_cross_attention_forms_bit_identical(batch, kw, opts):
     a, sa = _run(eng, dims, 0, **kw)
     b, sb = _run(eng, dims, 0, opts=opts, **kw)
     _same(a, sa, b, sb)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0)], ids=["greedy", "beam5"])
+def test_ring_columns_and_snake_order_bit_identical(batch, kw):
+    """64-column ring-GEMM tiles and the layer-alternating cross-attention item order change only the schedule:
+    each output keeps its K summation order and each attention item its arithmetic."""
+    dims, eng = batch
+    rows64 = (("decode_gemm.qkv", 64), ("decode_gemm.fc1", 64), ("decode_gemm.out", 32))
+    a, sa = _run(eng, dims, 0, opts=rows64, **kw)
+    b, sb = _run(eng, dims, 0, opts=rows64 + (("decode_gemm_cols.qkv", 64), ("decode_gemm_cols.fc1", 64),
+                                              ("decode_gemm_cols.out", 64), ("cross_attn_snake", 1)), **kw)
+    _same(a, sa, b, sb)
+    assert sum(len(r.tokens) for r in a) > W * 5
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0)], ids=["greedy", "beam5"])

@@ -152,22 +152,24 @@ int main(int argc, char** argv) {
     for (int pad : {0, 64}) {
       // pad: activation row stride K + pad (a 64-element pad moves consecutive rows to different L2 channels)
       const GemmA ap{dA, (long long)s.K + pad, 0, 0};
-      for (int rpb : {0, 32, 64, 96}) {
+      for (int rpb : {0, 32, 64, 96})
+      for (int cols : {32, 64}) {
+        if (cols == 64 && (pad || rpb == 0 || rpb > 64)) continue;
         for (int kr : {0, 640, 1280, 2560, 5120}) {
           if (kr > s.K || (kr > 0 && kr != s.K && s.K <= 1280)) continue;
           if (pad && kr != 0) continue;
           CK(hipMemsetAsync(dC, 0, cbytes, st));
-          if (!launch_dec_ring(ap, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb)) {
+          if (!launch_dec_ring(ap, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb, cols)) {
             std::printf("ring kr=%d rows=%d unsupported\n", kr, rpb);
             continue;
           }
           CK(hipStreamSynchronize(st));
           const double err = f32 || pad ? 0.0 : maxdiff();
           const double us = timeit([&](int r) {
-            launch_dec_ring(ap, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb);
+            launch_dec_ring(ap, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, rpb, cols);
           });
-          std::printf("%s N=%5d K=%5d  RING kr=%4d rows=%3d pad=%2d %7.2f us  %7.1f GB/s(W)  rel diff %.1e\n", s.name, s.N,
-                      s.K, kr, rpb, pad, us, wbytes / us / 1e3, err);
+          std::printf("%s N=%5d K=%5d  RING kr=%4d rows=%3d cols=%2d pad=%2d %7.2f us  %7.1f GB/s(W)  rel diff %.1e\n", s.name, s.N,
+                      s.K, kr, rpb, cols, pad, us, wbytes / us / 1e3, err);
         }
       }
     }

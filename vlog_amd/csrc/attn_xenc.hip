@@ -182,6 +182,7 @@ struct XAttnArgs {
   const float* escale;                   // F8: [slots][T] per-position scale (E[t] = e4m3[t] * escale[t])
   const int* hyp_slot; const int* row_hyp; const int* done;
   int H, T, d, G, n_mt, splits, n_items, per_xcd;
+  int rev;                               // 1: each XCD walks its items in reverse (see launch_xattn)
   long long slab_rows;                   // rows of the whole pass: partial slab stride
   bf16* part_u;                          // [splits][H][d/16][slab_rows][16]   u_s / l_s
   float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
@@ -446,7 +447,8 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   const int n_tiles = (a.T + 31) / 32;
   // XCD-aware item order: the blocks of one (group, split), i.e. its m-tiles, run on one XCD at about the
   // same time, so the 2nd..n-th reads of an E tile hit that XCD's L2
-  const int item = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
+  const int j = blockIdx.x >> 3;
+  const int item = (blockIdx.x & 7) * a.per_xcd + (a.rev ? a.per_xcd - 1 - j : j);
   if (item >= a.n_items) return;
   const int mt = item % a.n_mt;
   const int rest = item / a.n_mt;
@@ -677,7 +679,7 @@ static int g_xattn_abl = [] {            // ablation / load-policy experiments (
 void xattn_set_ablation(int abl) { g_xattn_abl = abl; }
 
 void launch_xattn(const bf16* qp, const void* enc, const float* escale, const int* hyp_slot, const int* row_hyp,
-                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, bf16* part_u,
+                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, int rev, bf16* part_u,
                   float* part_ml, float* probs, const int* head_map, int n_align, unsigned long long* stat,
                   hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
@@ -685,7 +687,7 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
   if (splits < 1 || splits > XMAXS || splits > (T + 31) / 32) throw std::runtime_error("xattn: bad key splits");
   XAttnArgs a{};
   a.qp = qp; a.enc = (const bf16*)enc; a.escale = escale; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
-  a.H = H; a.T = T; a.d = d; a.G = group; a.n_mt = (group * H + 31) / 32; a.splits = splits;
+  a.H = H; a.T = T; a.d = d; a.G = group; a.n_mt = (group * H + 31) / 32; a.splits = splits; a.rev = rev;
   const long long items = (long long)(rows / group) * a.n_mt * splits;
   if (items > (1LL << 30)) throw std::runtime_error("xattn: too many work items");
   a.n_items = (int)items;

@@ -47,7 +47,7 @@ void launch_xpack(const bf16*, bf16*, bf16*, int, int, int, hipStream_t);
 void launch_xq(const bf16*, long long, const CrossFuse&, const bf16*, bf16*, int, int, int, hipStream_t);
 int xattn_splits(int, int, int, int, int);
 void launch_xquant8(const bf16*, long long, int, unsigned char*, float*, hipStream_t);
-void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int,
+void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int, int,
                   bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, const float*, const int*, const int*, bf16*,
                      long long, int, int, int, int, int, float*, const int*, int, hipStream_t);
@@ -157,6 +157,7 @@ struct wm_engine {
   // Preset 1 (default) is the fastest per projection measured at 150 rows (tools/dec_gemm_bench);
   // preset 0 is round 1's routing.
   int dec_plan[6] = {96, 32, 32, 32, 0, -1};
+  int dec_cols[6] = {32, 32, 32, 32, 32, 32};   // ring GEMM output columns per block (32 or 64)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
@@ -165,6 +166,7 @@ struct wm_engine {
   // holds its encoder output, 3.84 MB for large-v3), 0 = projected cross-KV panels (attn_dec.hip: 245.8 MB
   // per large-v3 window, projected by wm_cross_kv)
   int cross_mode = 1;
+  bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
   DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs (cross_fp8: OCP e4m3 bytes)
   DevBuf xscale;             // cross_fp8: [n_slots][T] f32 per-position scales
   int cross_fp8 = 0;         // opt-in fp8 cross memory (factored form only; changes numerics, never the default)
@@ -502,7 +504,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     const int p = plan_of(proj);
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
-    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, K <= 1280 ? K : 1280, st, p)) return;
+    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, K <= 1280 ? K : 1280, st, p, e->dec_cols[proj])) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
     launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
@@ -570,7 +572,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     {
       ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
       launch_xattn(qp, e->xenc.p, e->cross_fp8 ? e->xscale.as<float>() : nullptr, e->d_hyp_slot.as<int>(), row_hyp, done, rows, sl.total_rows, cross_group, H, T,
-                   d, splits, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+                   d, splits, e->xsnake ? (l & 1) : 0, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
     }
     {
       ProfScope ps(e, P_CROSS_COMB, st, 2.0 * rows * d * d, 2.0 * d * d + 2.0 * splits * rows * prow + 2.0 * rows * d);
@@ -1160,7 +1162,8 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
       const int p = std::atoi(v) != 0;
       for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[p][i];
     }
-    if (const char* v = std::getenv("VLOG_AMD_DEC_GEMM")) {       // per projection, e.g. "qkv=32,fc2=64"
+    // per projection, e.g. VLOG_AMD_DEC_GEMM="qkv=32,fc2=64" (rows per block), VLOG_AMD_DEC_COLS="fc1=64"
+    auto per_proj = [](const char* v, int* dst) {
       std::string spec(v);
       size_t pos = 0;
       while (pos < spec.size()) {
@@ -1169,14 +1172,17 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
         const size_t eq = item.find('=');
         if (eq != std::string::npos)
           for (int i = 0; i < DEC_NPROJ; ++i)
-            if (item.substr(0, eq) == kDecProjNames[i]) e->dec_plan[i] = std::atoi(item.c_str() + eq + 1);
+            if (item.substr(0, eq) == kDecProjNames[i]) dst[i] = std::atoi(item.c_str() + eq + 1);
         pos = end + 1;
       }
-    }
+    };
+    if (const char* v = std::getenv("VLOG_AMD_DEC_GEMM")) per_proj(v, e->dec_plan);
+    if (const char* v = std::getenv("VLOG_AMD_DEC_COLS")) per_proj(v, e->dec_cols);
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_MODE")) e->cross_mode = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_XSNAKE")) e->xsnake = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
     try {
       build_layout(e);
@@ -1432,9 +1438,17 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
       if (i == DEC_NPROJ) throw std::runtime_error("wm_set_option: unknown projection " + pj);
       if (value < -2 || value > 160) throw std::runtime_error("wm_set_option: decode_gemm.<proj> in [-2, 160]");
       e->dec_plan[i] = (int)value;
+    } else if (k.rfind("decode_gemm_cols.", 0) == 0) {
+      const std::string pj = k.substr(17);
+      int i = 0;
+      while (i < DEC_NPROJ && pj != kDecProjNames[i]) ++i;
+      if (i == DEC_NPROJ) throw std::runtime_error("wm_set_option: unknown projection " + pj);
+      if (value != 32 && value != 64) throw std::runtime_error("wm_set_option: decode_gemm_cols.<proj> is 32 or 64");
+      e->dec_cols[i] = (int)value;
     }
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
+    else if (k == "cross_attn_snake") e->xsnake = value != 0;
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
     else if (k == "cross_fp8") {
       // fp8 (OCP e4m3) cross memory in the factored form; switching re-allocates the window slots (their

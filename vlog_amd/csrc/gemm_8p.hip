@@ -19,6 +19,7 @@
 //    every issuing wave's wait (RAW), and no DMA targets a buffer a wave may still read (WAR).
 #include "gemm.h"
 #include "gemm_epi.h"
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -40,12 +41,24 @@ __device__ __forceinline__ int p8_swz(int row, int ch) { return row * P8_BK + ((
 // 2-8 % slower on the encoder shapes and was dropped.)
 template <int KIND, int ABL = 0, bool EARLY = true>
 __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M,
-                                                         int N, int K, GemmEpi epi, int tiles_n) {
+                                                         int N, int K, GemmEpi epi, int tiles_n, int gm) {
   __shared__ __attribute__((aligned(16))) bf16 smem[P8_SMEM];
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm = wgid / tiles_n, tn = wgid - tm * tiles_n;
+  // tile order: each XCD walks a contiguous wgid range.  gm = 0: row tiles in order, all column tiles of a
+  // row tile together (A panel reused from L2, every W panel re-fetched per row tile).  gm > 0: groups of gm row
+  // tiles walked column by column, so ~32 co-resident blocks of one XCD share gm A panels and 32 / gm W panels.
+  int tm, tn;
+  if (gm > 0) {
+    const int per = gm * tiles_n, g = wgid / per, tiles_m = nwg / tiles_n;
+    const int gsz = min(gm, tiles_m - g * gm), j = wgid - g * per;
+    tm = g * gm + j % gsz;
+    tn = j / gsz;
+  } else {
+    tm = wgid / tiles_n;
+    tn = wgid - tm * tiles_n;
+  }
   const int m0 = tm * P8_BM, n0 = tn * P8_BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -285,6 +298,16 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
   }
 }
 
+// Row tiles per group of the tile order (VLOG_AMD_GEMM_GROUP; 0 = row-major order).  Schedule only: every tile's
+// arithmetic is the same in any order.
+static int gemm_8p_group() {
+  static const int v = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_GROUP");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return v;
+}
+
 template <int KIND>
 static void run_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st) {
   static const bool early = [] {
@@ -292,10 +315,11 @@ static void run_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, i
     return !(e && e[0] == '2');
   }();
   const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
+  const int gm = gemm_8p_group();
   if (early)
-    hipLaunchKernelGGL((gemm_8p_kernel<KIND, 0, true>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
+    hipLaunchKernelGGL((gemm_8p_kernel<KIND, 0, true>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gm);
   else
-    hipLaunchKernelGGL((gemm_8p_kernel<KIND, 0, false>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n);
+    hipLaunchKernelGGL((gemm_8p_kernel<KIND, 0, false>), dim3(tiles_m * tiles_n), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gm);
   WM_LAUNCH_CHECK("gemm_8p_kernel");
 }
 
@@ -319,13 +343,13 @@ void launch_gemm_8p_abl(const GemmA& a, const bf16* w, long long ldw, int M, int
   const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
   const dim3 g(tiles_m * tiles_n);
   switch (abl) {
-    case 0: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 0>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
-    case 1: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 1>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
-    case 2: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 2>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
-    case 3: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 3>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
-    case 4: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 4>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
-    case 5: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 5>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
-    case 7: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 7>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n); break;
+    case 0: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 0>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gemm_8p_group()); break;
+    case 1: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 1>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gemm_8p_group()); break;
+    case 2: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 2>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gemm_8p_group()); break;
+    case 3: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 3>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gemm_8p_group()); break;
+    case 4: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 4>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gemm_8p_group()); break;
+    case 5: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 5>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gemm_8p_group()); break;
+    case 7: hipLaunchKernelGGL((gemm_8p_kernel<EPI_BF16, 7>), g, dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, gemm_8p_group()); break;
     default: throw std::runtime_error("launch_gemm_8p_abl: bad ablation");
   }
 }

@@ -181,27 +181,29 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
-template <int MF, int KIND, int R, int PK = 1>
+template <int MF, int KIND, int R, int PK = 1, int NC = 1>
 __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
                                                        int K, GemmEpi epi, int tiles_n, int splitk, int kr,
                                                        float* __restrict__ part, int rgroups) {
   static_assert(MF % 2 == 0, "MF must be even");
-  // a ring slot holds PK consecutive 64-k sub-panels (one barrier per PK x 64 of K)
-  constexpr int ROWS = MF * 16, HALF = MF / 2, SUB = (ROWS + 32) * 64, SLOT = PK * SUB, DA = ROWS / 32,
-                DPP = PK * (DA + 1);
+  // a ring slot holds PK consecutive 64-k sub-panels (one barrier per PK x 64 of K); a block covers WR = 32 NC
+  // output columns (each wave NC fragments of 16)
+  constexpr int ROWS = MF * 16, HALF = MF / 2, WR = 32 * NC, SUB = (ROWS + WR) * 64, SLOT = PK * SUB, DA = ROWS / 32,
+                DPP = PK * (DA + NC);
   __shared__ __attribute__((aligned(16))) bf16 smem[R * SLOT];
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  // consecutive ids (one XCD) = the K splits and row groups of one 32-column tile: its weight panel is read from
+  // consecutive ids (one XCD) = the K splits and row groups of one column tile: its weight panel is read from
   // HBM once and served to the other row groups from that XCD's L2
   const int split = wgid % splitk, rg = (wgid / splitk) % rgroups, tile = wgid / (splitk * rgroups);
-  const int n0 = tile * 32, m0 = rg * ROWS;
+  const int n0 = tile * WR, m0 = rg * ROWS;
   const int kb = split * kr, klen = min(kr, K - kb), NS = klen / 64, NP = (NS + PK - 1) / PK;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid & 1, wr = wid >> 1;
 
-  // DMA sources: wave `wid` moves A rows [wid*ROWS/4, +ROWS/4) (DA instructions of 8 rows) and W rows [8 wid, +8)
+  // DMA sources: wave `wid` moves A rows [wid*ROWS/4, +ROWS/4) (DA instructions of 8 rows) and W rows
+  // [8 NC wid, +8 NC) (NC instructions)
   const bf16* srcA[DA];
 #pragma unroll
   for (int j = 0; j < DA; ++j) {
@@ -211,11 +213,12 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
     const long long off = a.rpb ? (long long)(gr / a.rpb) * a.bstride + (long long)(gr % a.rpb) * a.ld : (long long)gr * a.ld;
     srcA[j] = a.ptr + off + kb + ch * 8;
   }
-  const bf16* srcW;
-  {
-    const int row = wid * 8 + (lane >> 3);
+  const bf16* srcW[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int row = (wid * NC + j) * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    srcW = w + (long long)min(n0 + row, N - 1) * ldw + kb + ch * 8;
+    srcW[j] = w + (long long)min(n0 + row, N - 1) * ldw + kb + ch * 8;
   }
   // super-panel p = sub-panels [p PK, p PK + PK) (clamped to the last one: duplicates are never read)
   auto issue = [&](int p) {
@@ -227,14 +230,18 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
       for (int j = 0; j < DA; ++j)
         __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + sp * 64),
                                          (__attribute__((address_space(3))) void*)(s + (wid * (ROWS / 4) + j * 8) * 64), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(srcW + sp * 64),
-                                       (__attribute__((address_space(3))) void*)(s + (ROWS + wid * 8) * 64), 16, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(srcW[j] + sp * 64),
+                                         (__attribute__((address_space(3))) void*)(s + (ROWS + (wid * NC + j) * 8) * 64), 16, 0, 0);
     }
   };
 
-  f32x4 acc[HALF];
+  f32x4 acc[NC][HALF];
 #pragma unroll
-  for (int i = 0; i < HALF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) acc[c][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int pre = min(R - 1, NP);
   for (int p = 0; p < pre; ++p) issue(p);
   for (int p = 0; p < NP; ++p) {
@@ -248,12 +255,16 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ch = kk * 4 + (lane >> 4);
-        const bf16x8 fb = *(const bf16x8*)(sW + dswz(wc * 16 + (lane & 15), ch));
+        bf16x8 fb[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) fb[c] = *(const bf16x8*)(sW + dswz((wc * NC + c) * 16 + (lane & 15), ch));
         bf16x8 fa[HALF];
 #pragma unroll
         for (int i = 0; i < HALF; ++i) fa[i] = *(const bf16x8*)(sA + dswz((wr * HALF + i) * 16 + (lane & 15), ch));
 #pragma unroll
-        for (int i = 0; i < HALF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[i], 0, 0, 0);
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int i = 0; i < HALF; ++i) acc[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[c], fa[i], acc[c][i], 0, 0, 0);
       }
     };
     if (p * PK + PK <= NS) {              // a whole super-panel: no per-sub-panel branch in the MFMA stream
@@ -265,16 +276,19 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   }
 
   const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
-  const int col0 = n0 + wc * 16 + 4 * (lane >> 4);
-  if (col0 >= N) return;
 #pragma unroll
-  for (int i = 0; i < HALF; ++i) {
-    const int row = m0 + (wr * HALF + i) * 16 + (lane & 15);
-    if (row >= M) continue;
-    if (to_slab)
-      *(f32x4*)(part + ((long long)split * M + row) * N + col0) = acc[i];
-    else
-      apply_epi4<KIND>(epi, row, col0, acc[i]);
+  for (int c = 0; c < NC; ++c) {
+    const int col0 = n0 + (wc * NC + c) * 16 + 4 * (lane >> 4);
+    if (col0 >= N) continue;
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+      const int row = m0 + (wr * HALF + i) * 16 + (lane & 15);
+      if (row >= M) continue;
+      if (to_slab)
+        *(f32x4*)(part + ((long long)split * M + row) * N + col0) = acc[c][i];
+      else
+        apply_epi4<KIND>(epi, row, col0, acc[c][i]);
+    }
   }
 }
 
@@ -289,19 +303,19 @@ static int ring_pk() {
   return v;
 }
 
-template <int MF, int KIND>
+template <int MF, int KIND, int NC>
 static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      int splitk, int kr, hipStream_t st) {
-  constexpr int R = MF <= 4 ? 8 : MF <= 8 ? 7 : 6;     // (MF*16 + 32) * 128 B per slot, <= 144 KiB in all
-  constexpr int SUBB = (MF * 16 + 32) * 128;           // bytes of one 64-k sub-panel
+  constexpr int SUBB = (MF * 16 + 32 * NC) * 128;      // bytes of one 64-k sub-panel
+  constexpr int R = NC == 1 ? (MF <= 4 ? 8 : MF <= 8 ? 7 : 6) : std::min(8, (144 * 1024) / SUBB);   // <= 144 KiB
   constexpr int R2 = std::min(8, (144 * 1024) / (2 * SUBB)), R4 = std::min(8, (144 * 1024) / (4 * SUBB));
-  const int tiles_n = (N + 31) / 32;
+  const int tiles_n = (N + 32 * NC - 1) / (32 * NC);
   const int rgroups = (M + MF * 16 - 1) / (MF * 16);
   const dim3 grid(tiles_n * rgroups * splitk);
   const int pk = ring_pk();
   if constexpr (R4 >= 3) {
     if (pk == 4) {
-      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R4, 4>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R4, 4, NC>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
                          splitk, kr, ws, rgroups);
       WM_LAUNCH_CHECK("dec_ring_kernel");
       return;
@@ -309,14 +323,14 @@ static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   }
   if constexpr (R2 >= 3) {
     if (pk >= 2) {
-      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R2, 2>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R2, 2, NC>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
                          splitk, kr, ws, rgroups);
       WM_LAUNCH_CHECK("dec_ring_kernel");
       return;
     }
   }
-  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk, kr,
-                     ws, rgroups);
+  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R, 1, NC>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk,
+                     kr, ws, rgroups);
   WM_LAUNCH_CHECK("dec_ring_kernel");
 }
 
@@ -324,20 +338,30 @@ static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
 // and ceil(M / rows) row groups.
 template <int KIND>
 static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
-                          float* ws, int splitk, int kr, int rows_per_block, hipStream_t st) {
+                          float* ws, int splitk, int kr, int rows_per_block, int cols, hipStream_t st) {
   const int rows = rows_per_block > 0 ? std::min(rows_per_block, ((M + 31) / 32) * 32) : M;
-  if (rows <= 32) run_ring<2, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (rows <= 64) run_ring<4, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (rows <= 96) run_ring<6, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (rows <= 128) run_ring<8, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else run_ring<10, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  if (cols == 64) {                      // 64-column tiles: row groups of <= 64 (the ring slot must hold 3 x 2 sub-panels)
+    if (rows <= 32) run_ring<2, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    else if (rows <= 64) run_ring<4, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    else throw std::runtime_error("dec_ring: 64-column tiles take at most 64 rows per block");
+    return;
+  }
+  if (rows <= 32) run_ring<2, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (rows <= 64) run_ring<4, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (rows <= 96) run_ring<6, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (rows <= 128) run_ring<8, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_ring<10, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
 // Ring path: N % 4 == 0, K % 64 == 0; M <= 160 for one row group, any M with rows_per_block > 0.  kr = K range
-// per block (0: the whole K up to 1280, else split into ceil(K / 1280) ranges).  Returns false when unsupported.
+// per block (0: the whole K up to 1280, else split into ceil(K / 1280) ranges).  cols = output columns per block,
+// 32 or 64 (64: at most 64 rows per block).  A column tile's width never changes a row's K summation order, so
+// both widths give bit-identical results.  Returns false when unsupported.
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block) {
+                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block, int cols) {
   if ((rows_per_block <= 0 && M > 160) || rows_per_block > 160 || N % 4 != 0 || K % 64 != 0) return false;
+  if (cols != 32 && cols != 64) return false;
+  if (cols == 64 && (rows_per_block <= 0 ? M : std::min(rows_per_block, ((M + 31) / 32) * 32)) > 64) return false;
   if (kr <= 0) kr = K <= 1280 ? K : ((K + (K + 1279) / 1280 - 1) / ((K + 1279) / 1280) + 63) / 64 * 64;
   if (kr % 64 != 0) return false;
   const int splitk = (K + kr - 1) / kr;
@@ -346,11 +370,11 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   switch (epi.kind) {
-    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
-    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
-    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
-    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
-    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, st); break;
+    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
+    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
+    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
+    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
+    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
     default: return false;
   }
   if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
