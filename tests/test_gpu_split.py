@@ -42,9 +42,7 @@ def _run(eng, dims, split, opts=(), **kw):
     eng.set_option("cross_attn_fuse", 1)
     eng.set_option("cross_attn_blocks", 0)
     eng.set_option("cross_attn_snake", 0)
-    eng.set_option("decode_gemm_plan", 1)
-    for pj in ("qkv", "out", "cq", "cout", "fc1", "fc2"):
-        eng.set_option("decode_gemm_cols." + pj, 32)
+    eng.set_option("decode_gemm_plan", 1)          # also restores the preset's column widths
     return res, steps
 
 
@@ -73,7 +71,8 @@ def test_ring_columns_and_snake_order_bit_identical(batch, kw):
     each output keeps its K summation order and each attention item its arithmetic."""
     dims, eng = batch
     rows64 = (("decode_gemm.qkv", 64), ("decode_gemm.fc1", 64), ("decode_gemm.out", 32))
-    a, sa = _run(eng, dims, 0, opts=rows64, **kw)
+    cols32 = tuple(("decode_gemm_cols." + pj, 32) for pj in ("qkv", "fc1", "out"))
+    a, sa = _run(eng, dims, 0, opts=rows64 + cols32, **kw)
     b, sb = _run(eng, dims, 0, opts=rows64 + (("decode_gemm_cols.qkv", 64), ("decode_gemm_cols.fc1", 64),
                                               ("decode_gemm_cols.out", 64), ("cross_attn_snake", 1)), **kw)
     _same(a, sa, b, sb)

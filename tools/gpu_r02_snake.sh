@@ -8,6 +8,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_split.py -m gpu -x -v --tim
 for s in 0 1 0 1; do XB_SNAKE=$s XB_ABL=0 XB_F8=0 timeout -k 10 60 ./tools/xattn_bench 150 3 2 >> gpurun_out/${TAG}_micro.txt 2>&1 || exit 1; done
 cat gpurun_out/${TAG}_micro.txt
 for g in 0 4 8 0 4 8; do echo "GROUP=$g"; VLOG_AMD_GEMM_GROUP=$g timeout -k 10 120 ./tools/gemm_bench 10 2>&1 | head -5; done > gpurun_out/${TAG}_gemm.txt || exit 1; cat gpurun_out/${TAG}_gemm.txt
+GEMM_ABL=1 timeout -k 10 120 ./tools/gemm_bench 10 > gpurun_out/${TAG}_gemm_abl.txt 2>&1 || exit 1; grep abl= gpurun_out/${TAG}_gemm_abl.txt
 timeout -k 10 150 ./tools/dec_gemm_bench 200 150 > gpurun_out/${TAG}_dec.txt 2>&1 || exit 1; grep -E "RING|launch_gemm" gpurun_out/${TAG}_dec.txt
 i=0
 for kv in "BASE=1" "VLOG_AMD_XSNAKE=1" "VLOG_AMD_DEC_COLS=fc1=64:VLOG_AMD_DEC_GEMM=fc1=64" "VLOG_AMD_GEMM_GROUP=4" "VLOG_AMD_GEMM_GROUP=8" "VLOG_AMD_XSNAKE=1:VLOG_AMD_XABL=8" "BASE=1" "VLOG_AMD_XSNAKE=1" "VLOG_AMD_DEC_COLS=fc1=64:VLOG_AMD_DEC_GEMM=fc1=64" "VLOG_AMD_GEMM_GROUP=4"; do

@@ -108,7 +108,10 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Decoder projections (index of wm_engine::dec_plan)
 enum DecProj { DEC_QKV = 0, DEC_OUT, DEC_CQ, DEC_COUT, DEC_FC1, DEC_FC2, DEC_NPROJ };
 static const char* kDecProjNames[DEC_NPROJ] = {"qkv", "out", "cq", "cout", "fc1", "fc2"};
-static const int kDecPlanPresets[2][DEC_NPROJ] = {{0, -1, -1, -1, 0, -1}, {96, 32, 32, 32, 0, -1}};
+// preset 1 (default): per-projection fastest at 150 rows (tools/dec_gemm_bench, then bench.py A/B).  Round 2:
+// fc1 as 64-row x 64-column ring tiles (240 blocks of 320 KB instead of 160 of 480 KB: 12.4 -> 9.0 us).
+static const int kDecPlanPresets[2][DEC_NPROJ] = {{0, -1, -1, -1, 0, -1}, {96, 32, 32, 32, 64, -1}};
+static const int kDecColsPresets[2][DEC_NPROJ] = {{32, 32, 32, 32, 32, 32}, {32, 32, 32, 32, 64, 32}};
 
 // Decoder weight pointers per layer (resolved once: the arena layout is fixed at wm_create).
 struct DecLayerW {
@@ -156,8 +159,8 @@ struct wm_engine {
   //    -2  one-shot GEMM (gemm_dec.hip launch_dec_oneshot)
   // Preset 1 (default) is the fastest per projection measured at 150 rows (tools/dec_gemm_bench);
   // preset 0 is round 1's routing.
-  int dec_plan[6] = {96, 32, 32, 32, 0, -1};
-  int dec_cols[6] = {32, 32, 32, 32, 32, 32};   // ring GEMM output columns per block (32 or 64)
+  int dec_plan[6] = {96, 32, 32, 32, 64, -1};
+  int dec_cols[6] = {32, 32, 32, 32, 64, 32};   // ring GEMM output columns per block (32 or 64)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
@@ -1160,7 +1163,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_PLAN")) {
       const int p = std::atoi(v) != 0;
-      for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[p][i];
+      for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[p][i], e->dec_cols[i] = kDecColsPresets[p][i];
     }
     // per projection, e.g. VLOG_AMD_DEC_GEMM="qkv=32,fc2=64" (rows per block), VLOG_AMD_DEC_COLS="fc1=64"
     auto per_proj = [](const char* v, int* dst) {
@@ -1430,7 +1433,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
     else if (k == "decode_gemm_plan") {
       if (value != 0 && value != 1) throw std::runtime_error("wm_set_option: decode_gemm_plan is 0 or 1");
-      for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[value][i];
+      for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[value][i], e->dec_cols[i] = kDecColsPresets[value][i];
     } else if (k.rfind("decode_gemm.", 0) == 0) {
       const std::string pj = k.substr(12);
       int i = 0;
