@@ -202,12 +202,15 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   split-K skinny GEMM).
  *   "decode_gemm_plan" (default 1): preset routing of the six decoder projections (qkv, out, cq, cout, fc1, fc2)
  *   for passes of <= 1024 rows; 0 = round-1 routing (ring for qkv/fc1, skinny split-K for the rest), 1 = the
- *   per-projection fastest at 150 rows (tools/dec_gemm_bench; fc1 as 64 x 64 ring tiles).  "decode_gemm.<proj>" sets one projection:
+ *   per-projection fastest at 150 rows (tools/dec_gemm_bench; fc1 and fc2 as 64 x 64 ring tiles).  "decode_gemm.<proj>" sets one projection:
  *   > 0 ring GEMM with the rows in groups of that many, 0 all-rows ring, -1 skinny split-K, -2 one-shot GEMM.
  *   Routes differ in K summation order (results agree to f32 rounding, not bit for bit).
- *   "decode_gemm_cols.<proj>" (preset 1: 64 for fc1, else 32): output columns per ring-GEMM block, 32 or 64 (64
+ *   "decode_gemm_cols.<proj>" (preset 1: 64 for fc1 and fc2, else 32): output columns per ring-GEMM block, 32 or 64 (64
  *   takes row groups of at most 64; other routes ignore it).  Bit-identical either way.  decode_gemm_plan also
  *   resets these to its preset.
+ *   "gemm_persistent" (default 1, process-wide): large encoder GEMMs run as one persistent block per CU walking
+ *   its tiles, the next tile's first K-tiles loaded during the current tile's last K-steps and epilogue; 0 = one
+ *   block per tile.  Bit-identical.
  *   "cross_attn_snake" (default 0): odd decoder layers walk the factored cross-attention's items in reverse, so
  *   the encoder output read last by one layer is read first by the next (Infinity Cache reuse).  Bit-identical.
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its

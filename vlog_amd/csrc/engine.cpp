@@ -109,9 +109,11 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 enum DecProj { DEC_QKV = 0, DEC_OUT, DEC_CQ, DEC_COUT, DEC_FC1, DEC_FC2, DEC_NPROJ };
 static const char* kDecProjNames[DEC_NPROJ] = {"qkv", "out", "cq", "cout", "fc1", "fc2"};
 // preset 1 (default): per-projection fastest at 150 rows (tools/dec_gemm_bench, then bench.py A/B).  Round 2:
-// fc1 as 64-row x 64-column ring tiles (240 blocks of 320 KB instead of 160 of 480 KB: 12.4 -> 9.0 us).
-static const int kDecPlanPresets[2][DEC_NPROJ] = {{0, -1, -1, -1, 0, -1}, {96, 32, 32, 32, 64, -1}};
-static const int kDecColsPresets[2][DEC_NPROJ] = {{32, 32, 32, 32, 32, 32}, {32, 32, 32, 32, 64, 32}};
+// fc1 as 64-row x 64-column ring tiles (240 blocks of 320 KB instead of 160 of 480 KB: 12.4 -> 9.0 us) and fc2
+// likewise (K split in 4 ranges of 1280, slabs summed by the residual+LayerNorm combine: 16.1 -> 13.8 us with the
+// combine); bench.py on one box: dec_gemm 372 -> 352 (fc1) -> 341-343 ms/step (fc2).
+static const int kDecPlanPresets[2][DEC_NPROJ] = {{0, -1, -1, -1, 0, -1}, {96, 32, 32, 32, 64, 64}};
+static const int kDecColsPresets[2][DEC_NPROJ] = {{32, 32, 32, 32, 32, 32}, {32, 32, 32, 32, 64, 64}};
 
 // Decoder weight pointers per layer (resolved once: the arena layout is fixed at wm_create).
 struct DecLayerW {
@@ -159,8 +161,8 @@ struct wm_engine {
   //    -2  one-shot GEMM (gemm_dec.hip launch_dec_oneshot)
   // Preset 1 (default) is the fastest per projection measured at 150 rows (tools/dec_gemm_bench);
   // preset 0 is round 1's routing.
-  int dec_plan[6] = {96, 32, 32, 32, 64, -1};
-  int dec_cols[6] = {32, 32, 32, 32, 64, 32};   // ring GEMM output columns per block (32 or 64)
+  int dec_plan[6] = {96, 32, 32, 32, 64, 64};
+  int dec_cols[6] = {32, 32, 32, 32, 64, 64};   // ring GEMM output columns per block (32 or 64)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
@@ -1452,6 +1454,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else if (k == "cross_attn_snake") e->xsnake = value != 0;
+    else if (k == "gemm_persistent") gemm_8p_set_persistent((int)value);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
     else if (k == "cross_fp8") {
       // fp8 (OCP e4m3) cross memory in the factored form; switching re-allocates the window slots (their

@@ -263,6 +263,18 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
     float* sf = (float*)smem;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
+      // RESID_F32: this thread's 16 residual chunks of the half are loaded before the staging (one memory round
+      // trip, overlapping the LDS writes and the barrier) instead of four dependent batches in the store loop;
+      // the accumulators of half 0 are dead by then, so the 64 registers are free
+      f32x4 res[16];
+      if (KIND == EPI_RESID_F32) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int c = tid + 512 * k, rl = c >> 6, cc = (c & 63) * 4;
+          const int row = min(m0 + half * 128 + rl, M - 1), col0 = min(n0 + cc, N - 4);
+          res[k] = *(const f32x4*)((const float*)epi.out + (long long)row * epi.ldc + col0);
+        }
+      }
       if (wm == half) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -276,11 +288,15 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
         }
       }
       __syncthreads();
-#pragma unroll 4
+#pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int c = tid + 512 * k, rl = c >> 6, cc = (c & 63) * 4;
         const int row = m0 + half * 128 + rl, col0 = n0 + cc;
-        if (row < M && col0 < N) epi_store4_f32<KIND>(epi, row, col0, *(const f32x4*)(sf + rl * P8_SR32 + cc));
+        if (row < M && col0 < N) {
+          const f32x4 v = *(const f32x4*)(sf + rl * P8_SR32 + cc);
+          if (KIND == EPI_RESID_F32) *(f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0) = res[k] + v;
+          else epi_store4_f32<KIND>(epi, row, col0, v);
+        }
       }
       __syncthreads();
     }
@@ -298,6 +314,250 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
   }
 }
 
+// ------------------------------------------------------------------------------------------------------
+// Persistent form (the default for large encoder GEMMs with contiguous A): one block per CU walks a sequence of
+// output tiles.  The K-step stream runs on across tile seams: in the last two K-steps of a tile, the slots that
+// would prefetch K-tiles t+2 instead take the NEXT tile's K-tiles 0 and 1 (same buffers, same phases, same
+// counted waits as inside a tile), so a new tile starts with its operands already in LDS instead of paying a
+// DMA round trip.  The epilogue stages through a 32 KiB region beside the two 64 KiB operand buffers (64-row
+// passes for bf16, 32-row passes for f32, 16-B chunks XOR-swizzled by row & 15: conflict-free for the fragment
+// writes and the whole-row reads), so it runs while the next tile's operands land, and its stores drain behind
+// the next tile's first K-step (the counted vmcnt there retires them with the K-tile-1 DMA).  RESID_F32 loads
+// the residual of pass p + 1 while pass p is stored.  Every tile's arithmetic is the non-persistent kernel's.
+#define PP_STAGE (2 * P8_BUF)                      // bf16-element offset of the staging region (128 KiB)
+#define PP_SMEM (PP_STAGE + 16384)                 // + 32 KiB = 160 KiB
+
+template <int KIND>
+__global__ __launch_bounds__(512, 1) void gemm_8pp_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M,
+                                                          int N, int K, GemmEpi epi, int tiles_n, int n_tiles) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[PP_SMEM];
+  const int bid = blockIdx.x, npx = gridDim.x >> 3;
+  const int xcd = bid & 7, jb = bid >> 3;
+  // this XCD's contiguous tile range (row tiles in order, all column tiles of a row tile together), walked by
+  // the XCD's npx blocks in lockstep rounds: co-resident blocks share A panels in the XCD's L2
+  const int q = n_tiles >> 3, r8 = n_tiles & 7;
+  const int start = xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q;
+  const int size = q + (xcd < r8 ? 1 : 0);
+  const int cnt = jb < size ? (size - jb + npx - 1) / npx : 0;
+  if (cnt == 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / P8_BK;
+
+  // quarter qq of K-tile kt of the tile at (m0, n0) -> buffer buf (same row/chunk mapping as gemm_8p_kernel)
+  auto dma = [&](int qq, int m0, int n0, int kt, int buf) {
+    int lo = lane;
+    asm volatile("" : "+v"(lo));           // recomputed per issue: no per-lane address kept live across the loop
+    bf16* dst = smem + buf * P8_BUF + (qq >> 1) * P8_TILE + ((qq & 1) * 128 + wid * 16) * P8_BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (qq & 1) * 128 + wid * 16 + j * 8 + (lo >> 3);
+      const int ch = (lo & 7) ^ ((row >> 1) & 7);
+      const bf16* src;
+      if (qq < 2) src = a.ptr + (long long)min(m0 + row, M - 1) * a.ld + ch * 8 + kt * P8_BK;
+      else src = w + (long long)min(n0 + row, N - 1) * ldw + ch * 8 + kt * P8_BK;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(dst + j * 8 * P8_BK), 16,
+                                       0, 0);
+    }
+  };
+  auto tile_mn = [&](int i, int& m0, int& n0) {
+    const int t = start + jb + npx * i;
+    const int tm = t / tiles_n;
+    m0 = tm * P8_BM;
+    n0 = (t - tm * tiles_n) * P8_BN;
+  };
+
+  int m0, n0;
+  tile_mn(0, m0, n0);
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) dma(qq, m0, n0, 0, 0);
+  if (nk > 1) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) dma(qq, m0, n0, 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  int g = 0;                                        // K-steps done by this block (buffer parity)
+  for (int i = 0; i < cnt; ++i) {
+    if (i > 0) tile_mn(i, m0, n0);
+    int m1 = 0, n1 = 0;
+    const bool has_next = i + 1 < cnt;
+    if (has_next) tile_mn(i + 1, m1, n1);
+    if (wm == 1) asm volatile("s_barrier" ::: "memory");   // stagger: group 1 runs one barrier behind
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[4][2], fb[2][2], fb2[2][2];
+    auto read_a = [&](const bf16* sA, int half) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          fa[ii][kk] = *(const bf16x8*)(sA + p8_swz(wm * 128 + half * 64 + ii * 16 + fr, kk * 4 + fq));
+    };
+    auto read_b = [&](const bf16* sB, int half, bf16x8 (&dst)[2][2]) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          dst[jj][kk] = *(const bf16x8*)(sB + p8_swz(wn * 64 + half * 32 + jj * 16 + fr, kk * 4 + fq));
+    };
+    auto mfma_q = [&](int ha, int hb, const bf16x8 (&fbx)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[ha * 4 + ii][hb * 2 + jj] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbx[jj][kk], fa[ii][kk], acc[ha * 4 + ii][hb * 2 + jj], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+#define PP_READ_DONE()                                          \
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+  __builtin_amdgcn_sched_barrier(0);
+#define PP_MFMA_DONE()                                          \
+  __builtin_amdgcn_sched_barrier(0);                            \
+  asm volatile("s_barrier" ::: "memory");
+    for (int t = 0; t < nk; ++t, ++g) {
+      const bf16* sA = smem + (g & 1) * P8_BUF;
+      const bf16* sB = sA + P8_TILE;
+      // the K-tile two steps ahead: this tile's t + 2, else the next tile's t + 2 - nk (0 or 1)
+      const bool in_tile = t + 2 < nk;
+      const bool more2 = in_tile || (has_next && t + 2 - nk < nk);
+      const int tm0 = in_tile ? m0 : m1, tn0 = in_tile ? n0 : n1, tk = in_tile ? t + 2 : t + 2 - nk;
+      read_b(sB, 0, fb);                                // phase 0: Q00
+      read_a(sA, 0);
+      PP_READ_DONE();
+      mfma_q(0, 0, fb);
+      PP_MFMA_DONE();
+      read_b(sB, 1, fb2);                               // phase 1: Q01
+      PP_READ_DONE();
+      mfma_q(0, 1, fb2);
+      PP_MFMA_DONE();
+      read_a(sA, 1);                                    // phase 2: Q11 + W of the K-tile two steps ahead
+      if (more2) { dma(2, tm0, tn0, tk, g & 1); dma(3, tm0, tn0, tk, g & 1); }
+      PP_READ_DONE();
+      mfma_q(1, 1, fb2);
+      PP_MFMA_DONE();
+      if (more2) {                                      // phase 3: Q10 + its A
+        dma(0, tm0, tn0, tk, g & 1);
+        dma(1, tm0, tn0, tk, g & 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      PP_READ_DONE();
+      mfma_q(1, 0, fb);
+      PP_MFMA_DONE();
+    }
+#undef PP_READ_DONE
+#undef PP_MFMA_DONE
+    if (wm == 0) asm volatile("s_barrier" ::: "memory");   // balance the stagger
+
+    // ---- epilogue through the 32 KiB staging region
+    char* stg = (char*)(smem + PP_STAGE);
+    constexpr bool BF16_OUT = KIND == EPI_BF16;
+    if (BF16_OUT) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {                     // rows [64 p, 64 p + 64): wave group p >> 1, fragments 4 (p & 1) ..
+        if (wm == (p >> 1)) {
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int i = (p & 1) * 4 + ii, rl = ii * 16 + fr;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int cl = wn * 64 + jj * 16 + 4 * fq;
+              const f32x4 v = epi_value4<KIND>(epi, m0 + wm * 128 + i * 16 + fr, min(n0 + cl, N - 4), acc[i][jj]);
+              bf16x4 o;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+              *(bf16x4*)(stg + rl * 512 + (((cl >> 3) ^ (rl & 15)) << 4) + ((cl >> 2) & 1) * 8) = o;
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = tid + 512 * k, rl = c >> 5, ch = c & 31;
+          const int row = m0 + p * 64 + rl, col0 = n0 + ch * 8;
+          const bf16x8 v = *(const bf16x8*)(stg + rl * 512 + ((ch ^ (rl & 15)) << 4));
+          if (row < M && col0 < N) epi_store8_bf16<KIND>(epi, row, col0, v);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
+      }
+    } else {
+      f32x4 rn[4];                                      // RESID_F32: residual chunks of the next pass
+      auto load_res = [&](int p, f32x4 (&dst)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = tid + 512 * k, rl = c >> 6, cc = (c & 63) * 4;
+          const int row = min(m0 + p * 32 + rl, M - 1), col0 = min(n0 + cc, N - 4);
+          dst[k] = *(const f32x4*)((const float*)epi.out + (long long)row * epi.ldc + col0);
+        }
+      };
+      if (KIND == EPI_RESID_F32) load_res(0, rn);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {                     // rows [32 p, 32 p + 32): wave group p >> 2, fragments 2 (p & 3) ..
+        f32x4 rc[4];
+        if (KIND == EPI_RESID_F32) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) rc[k] = rn[k];
+          if (p + 1 < 8) load_res(p + 1, rn);
+        }
+        if (wm == (p >> 2)) {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) {
+            const int i = (p & 3) * 2 + ii, rl = ii * 16 + fr;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int cl = wn * 64 + jj * 16 + 4 * fq;
+              *(f32x4*)(stg + rl * 1024 + (((cl >> 2) ^ (rl & 15)) << 4)) =
+                  epi_value4<KIND>(epi, m0 + wm * 128 + i * 16 + fr, min(n0 + cl, N - 4), acc[i][jj]);
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = tid + 512 * k, rl = c >> 6, ch = c & 63;
+          const int row = m0 + p * 32 + rl, col0 = n0 + ch * 4;
+          const f32x4 v = *(const f32x4*)(stg + rl * 1024 + ((ch ^ (rl & 15)) << 4));
+          if (row < M && col0 < N) {
+            if (KIND == EPI_RESID_F32) *(f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0) = rc[k] + v;
+            else epi_store4_f32<KIND>(epi, row, col0, v);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
+      }
+    }
+  }
+}
+
+// Process-wide (the GEMM launchers carry no engine): VLOG_AMD_GEMM_PERSIST=0 or wm_set_option("gemm_persistent", 0)
+// restores the one-tile-per-block kernel.  Bit-identical either way.
+static int g_gemm_persist = [] {
+  const char* e = std::getenv("VLOG_AMD_GEMM_PERSIST");
+  return e ? std::atoi(e) : 1;
+}();
+static int gemm_8p_persistent() { return g_gemm_persist; }
+void gemm_8p_set_persistent(int on) { g_gemm_persist = on != 0; }
+
+static int device_cus() {
+  static const int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return v;
+}
+
 // Row tiles per group of the tile order (VLOG_AMD_GEMM_GROUP; 0 = row-major order).  Schedule only: every tile's
 // arithmetic is the same in any order.
 static int gemm_8p_group() {
@@ -310,6 +570,18 @@ static int gemm_8p_group() {
 
 template <int KIND>
 static void run_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st) {
+  {
+    constexpr bool PK = KIND == EPI_BF16 || KIND == EPI_RESID_F32 || KIND == EPI_F32 || KIND == EPI_GELU_POS_F32;
+    const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
+    const int n_tiles = tiles_m * tiles_n, cus = device_cus();
+    const bool out_ok = KIND == EPI_BF16 ? (N % 8 == 0 && epi.ldc % 8 == 0 && (epi.rpb == 0 || epi.bstride % 8 == 0))
+                                         : epi.ldc % 4 == 0;
+    if (PK && gemm_8p_persistent() && a.rpb == 0 && out_ok && cus % 8 == 0 && n_tiles >= 2 * cus && K >= 2 * P8_BK && gemm_8p_group() == 0) {
+      hipLaunchKernelGGL((gemm_8pp_kernel<KIND>), dim3(cus), dim3(512), 0, st, a, w, ldw, M, N, K, epi, tiles_n, n_tiles);
+      WM_LAUNCH_CHECK("gemm_8pp_kernel");
+      return;
+    }
+  }
   static const bool early = [] {
     const char* e = std::getenv("VLOG_AMD_GEMM_8P");
     return !(e && e[0] == '2');
