@@ -208,9 +208,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_gemm_cols.<proj>" (preset 1: 64 for fc1 and fc2, else 32): output columns per ring-GEMM block, 32 or 64 (64
  *   takes row groups of at most 64; other routes ignore it).  Bit-identical either way.  decode_gemm_plan also
  *   resets these to its preset.
- *   "gemm_persistent" (default 1, process-wide): large encoder GEMMs run as one persistent block per CU walking
- *   its tiles, the next tile's first K-tiles loaded during the current tile's last K-steps and epilogue; 0 = one
- *   block per tile.  Bit-identical.
+ *   "gemm_persistent" (default 0, process-wide): 1 runs large encoder GEMMs as one persistent block per CU
+ *   walking its tiles, the next tile's first K-tiles loaded during the current tile's last K-steps and epilogue
+ *   (measured no faster than one block per tile).  Bit-identical.
  *   "cross_attn_snake" (default 0): odd decoder layers walk the factored cross-attention's items in reverse, so
  *   the encoder output read last by one layer is read first by the next (Infinity Cache reuse).  Bit-identical.
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its

@@ -29,7 +29,7 @@ def test_persistent_encoder_gemm_bit_identical():
         eng.set_option("gemm_persistent", 1)
         got = eng.encode(feats, seek, n)
     finally:
-        eng.set_option("gemm_persistent", 1)
+        eng.set_option("gemm_persistent", 0)
     torch.cuda.synchronize()
     assert got.shape == ref.shape and torch.isfinite(got.float()).all()
     assert torch.equal(got, ref)

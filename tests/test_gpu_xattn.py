@@ -11,10 +11,12 @@ import pytest
 import torch
 
 from oracle import mel as omel
+from oracle.decode import GenerateOptions
 from oracle.model import OracleWhisper
 from vlog_amd.audio import speech_like
 from vlog_amd.dims import model_dims
 from vlog_amd.weights import round_bf16, synthetic_state_dict
+from tests.parity_util import window_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -91,7 +93,21 @@ def test_factored_generate_matches_projected(small_models, kw):
 
     (ra, sa), (rb, sb) = _both(eng, enc, W, 5 * W, run)
     same = sum(x.tokens == y.tokens for x, y in zip(ra, rb))
-    assert same >= W - 1, f"{same}/{W} windows identical"
+    if kw:
+        assert same >= W - 1, f"{same}/{W} windows identical"
+    else:
+        # greedy on random weights: a window may flip at a near-tied step (bf16 noise between the two forms);
+        # then BOTH forms must be epsilon-consistent under the oracle, tie-aware (tests/parity_util.py)
+        eps = {"tiny": 0.02, "base": 0.03, "small": 0.05}[dims.name]
+        opt = GenerateOptions(beam_size=1, suppress_tokens=_sup(st), max_length=100)
+        encf = enc.float().cpu().numpy()
+        orc16 = OracleWhisper(orc.w, dims, np.float32, bf16_acts=True)     # the engine's numeric format
+        for w, (x, y) in enumerate(zip(ra, rb)):
+            if x.tokens != y.tokens:
+                for r in (x, y):
+                    wp = window_parity(orc16, encf[w], prompt, r, st, opt, w, eps=eps)
+                    assert wp.min_margin_rule_tie >= -eps, (w, wp.min_margin_rule_tie, wp.worst_step)
+        assert same >= W // 2, f"{same}/{W} windows identical"
     for x, y in zip(ra, rb):
         assert abs(x.no_speech_prob - y.no_speech_prob) < 2e-3
         if x.tokens == y.tokens:

@@ -472,14 +472,17 @@ struct XCombArgs {
 // partial and weight loads are issued KB k-steps at a time (one memory round trip per batch, not per
 // k-step).  The merged u is split into bf16 hi + lo parts (two MFMAs), so the V projection sees u to
 // ~16 bits instead of 8.  The 8 partial products are summed through LDS in a fixed order.
-template <int KS8, int MAXS>
+// RT = rows per block, 32 or 16.  With 16, MFMA rows 16..31 repeat rows 0..15 (same addresses: no extra bytes)
+// and are not stored, so every output keeps the 32-row form's arithmetic bit for bit while the grid doubles
+// (a block's partial bytes halve; the Wv_h panel is the same).
+template <int KS8, int MAXS, int RT = 32>
 __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
   constexpr int KB = (16 / MAXS) < KS8 ? (16 / MAXS) : KS8;   // k-steps per load batch (<= 16 partial loads)
   __shared__ float sR[8][2][16][64];
   __shared__ float sML[32][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
   const int h = blockIdx.y;
-  const int r = blockIdx.x * 32 + l32;
+  const int r = blockIdx.x * RT + (l32 & (RT - 1));
   const int rc = min(r, a.rows - 1);
   const long long sstride = a.slab_rows * a.H;          // (row, head) pairs per split slab
   float w[MAXS];
@@ -561,16 +564,18 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
 #pragma unroll
     for (int w2 = 1; w2 < 8; ++w2) v += sR[w2][jt][i][ln];
     const int j = 32 * jt + (ln & 31);
-    const int rr = blockIdx.x * 32 + 8 * (i >> 2) + 4 * (ln >> 5) + (i & 3);
+    const int tr = 8 * (i >> 2) + 4 * (ln >> 5) + (i & 3);
+    if (tr >= RT) continue;
+    const int rr = blockIdx.x * RT + tr;
     if (rr < a.rows && !(a.done && a.done[a.row_hyp[rr]]))
       a.out[(long long)rr * a.ldo + h * 64 + j] = f2bf(v + a.bv[h * 64 + j]);
   }
   if (a.probs) {
     const int hm = a.head_map[h];
     if (hm >= 0) {
-      for (int idx = tid; idx < 32 * a.T; idx += 512) {
+      for (int idx = tid; idx < RT * a.T; idx += 512) {
         const int ri = idx / a.T, t = idx - ri * a.T;
-        const int rr = blockIdx.x * 32 + ri;
+        const int rr = blockIdx.x * RT + ri;
         if (rr >= a.rows) continue;
         float* p = a.probs + ((long long)rr * a.n_align + hm) * a.T + t;
         *p = __builtin_amdgcn_exp2f(*p - sML[ri][0]) / sML[ri][1];
@@ -761,13 +766,22 @@ void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long 
   a.part_u = part_u; a.part_ml = part_ml; a.splits = splits; a.slab_rows = slab_rows; a.wvb = wvb; a.bv = bv;
   a.row_hyp = row_hyp; a.done = done; a.out = out; a.ldo = ldo; a.rows = rows; a.H = H; a.d = d; a.T = T;
   a.probs = probs; a.head_map = head_map; a.n_align = n_align;
-  const dim3 grid((rows + 31) / 32, H);
+  // 16-row blocks unless the grid already fills the chip with 32-row ones (VLOG_AMD_XCOMB_RT=32|16 forces)
+  static const int rt_forced = [] {
+    const char* e = std::getenv("VLOG_AMD_XCOMB_RT");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int rt = rt_forced == 16 || rt_forced == 32 ? rt_forced : ((rows + 31) / 32 * H >= 256 ? 32 : 16);
+  const dim3 grid((rows + rt - 1) / rt, H);
+#define XC_RT(KS8_, MS_)                                                                                          \
+  if (rt == 16) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 16>), grid, dim3(512), 0, st, a);                  \
+  else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 32>), grid, dim3(512), 0, st, a);
 #define XC_LAUNCH(KS8_)                                                                                  \
-  if (splits <= 1) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 1>), grid, dim3(512), 0, st, a);             \
-  else if (splits <= 2) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 2>), grid, dim3(512), 0, st, a);        \
-  else if (splits <= 4) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 4>), grid, dim3(512), 0, st, a);        \
-  else if (splits <= 8) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, 8>), grid, dim3(512), 0, st, a);        \
-  else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, XMAXS>), grid, dim3(512), 0, st, a);
+  if (splits <= 1) { XC_RT(KS8_, 1) }                                                                    \
+  else if (splits <= 2) { XC_RT(KS8_, 2) }                                                               \
+  else if (splits <= 4) { XC_RT(KS8_, 4) }                                                               \
+  else if (splits <= 8) { XC_RT(KS8_, 8) }                                                               \
+  else { XC_RT(KS8_, XMAXS) }
   switch (d) {                           // 8 waves x d/8 columns of the reduction: d/128 k-steps each
     case 384: XC_LAUNCH(3); break;
     case 512: XC_LAUNCH(4); break;
@@ -777,5 +791,6 @@ void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long 
     default: throw std::runtime_error("xcomb_vo: unsupported n_state " + std::to_string(d));
   }
 #undef XC_LAUNCH
+#undef XC_RT
   WM_LAUNCH_CHECK("xcomb_vo_kernel");
 }

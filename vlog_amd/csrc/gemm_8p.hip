@@ -315,7 +315,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
 }
 
 // ------------------------------------------------------------------------------------------------------
-// Persistent form (the default for large encoder GEMMs with contiguous A): one block per CU walks a sequence of
+// Persistent form (opt-in, gemm_persistent; large GEMMs with contiguous A): one block per CU walks a sequence of
 // output tiles.  The K-step stream runs on across tile seams: in the last two K-steps of a tile, the slots that
 // would prefetch K-tiles t+2 instead take the NEXT tile's K-tiles 0 and 1 (same buffers, same phases, same
 // counted waits as inside a tile), so a new tile starts with its operands already in LDS instead of paying a
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
 // passes for bf16, 32-row passes for f32, 16-B chunks XOR-swizzled by row & 15: conflict-free for the fragment
 // writes and the whole-row reads), so it runs while the next tile's operands land, and its stores drain behind
 // the next tile's first K-step (the counted vmcnt there retires them with the K-tile-1 DMA).  RESID_F32 loads
-// the residual of pass p + 1 while pass p is stored.  Every tile's arithmetic is the non-persistent kernel's.
+// the residual of pass p + 1 while pass p is stored.  Every output's arithmetic is the non-persistent kernel's.
 #define PP_STAGE (2 * P8_BUF)                      // bf16-element offset of the staging region (128 KiB)
 #define PP_SMEM (PP_STAGE + 16384)                 // + 32 KiB = 160 KiB
 
@@ -345,18 +345,32 @@ __global__ __launch_bounds__(512, 1) void gemm_8pp_kernel(GemmA a, const bf16* _
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = K / P8_BK;
 
-  // quarter qq of K-tile kt of the tile at (m0, n0) -> buffer buf (same row/chunk mapping as gemm_8p_kernel)
-  auto dma = [&](int qq, int m0, int n0, int kt, int buf) {
+  // DMA sources of the tile being streamed: uniform 64-bit bases (scalar registers) + per-lane 32-bit offsets
+  // (rows clamped to the matrix), switched to the next tile once, when the K-step stream crosses the seam.
+  // quarter qq of K-tile kt -> buffer buf: the same row/chunk mapping as gemm_8p_kernel.
+  const bf16* baseA = a.ptr;
+  const bf16* baseW = w;
+  int offA[2][2], offW[2][2];
+  auto set_src = [&](int tm0, int tn0) {
     int lo = lane;
-    asm volatile("" : "+v"(lo));           // recomputed per issue: no per-lane address kept live across the loop
+    asm volatile("" : "+v"(lo));
+    baseA = a.ptr + (long long)tm0 * a.ld;
+    baseW = w + (long long)tn0 * ldw;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = h * 128 + wid * 16 + j * 8 + (lo >> 3);
+        const int ch = (lo & 7) ^ ((row >> 1) & 7);
+        offA[h][j] = (min(tm0 + row, M - 1) - tm0) * (int)a.ld + ch * 8;
+        offW[h][j] = (min(tn0 + row, N - 1) - tn0) * (int)ldw + ch * 8;
+      }
+  };
+  auto dma = [&](int qq, int kt, int buf) {
     bf16* dst = smem + buf * P8_BUF + (qq >> 1) * P8_TILE + ((qq & 1) * 128 + wid * 16) * P8_BK;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int row = (qq & 1) * 128 + wid * 16 + j * 8 + (lo >> 3);
-      const int ch = (lo & 7) ^ ((row >> 1) & 7);
-      const bf16* src;
-      if (qq < 2) src = a.ptr + (long long)min(m0 + row, M - 1) * a.ld + ch * 8 + kt * P8_BK;
-      else src = w + (long long)min(n0 + row, N - 1) * ldw + ch * 8 + kt * P8_BK;
+      const bf16* src = (qq < 2 ? baseA + offA[qq & 1][j] : baseW + offW[qq & 1][j]) + kt * P8_BK;
       __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(dst + j * 8 * P8_BK), 16,
                                        0, 0);
     }
@@ -370,11 +384,12 @@ __global__ __launch_bounds__(512, 1) void gemm_8pp_kernel(GemmA a, const bf16* _
 
   int m0, n0;
   tile_mn(0, m0, n0);
+  set_src(m0, n0);
 #pragma unroll
-  for (int qq = 0; qq < 4; ++qq) dma(qq, m0, n0, 0, 0);
+  for (int qq = 0; qq < 4; ++qq) dma(qq, 0, 0);
   if (nk > 1) {
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) dma(qq, m0, n0, 1, 1);
+    for (int qq = 0; qq < 4; ++qq) dma(qq, 1, 1);
     asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -429,8 +444,9 @@ __global__ __launch_bounds__(512, 1) void gemm_8pp_kernel(GemmA a, const bf16* _
       const bf16* sB = sA + P8_TILE;
       // the K-tile two steps ahead: this tile's t + 2, else the next tile's t + 2 - nk (0 or 1)
       const bool in_tile = t + 2 < nk;
-      const bool more2 = in_tile || (has_next && t + 2 - nk < nk);
-      const int tm0 = in_tile ? m0 : m1, tn0 = in_tile ? n0 : n1, tk = in_tile ? t + 2 : t + 2 - nk;
+      const bool more2 = in_tile || has_next;
+      const int tk = in_tile ? t + 2 : t + 2 - nk;
+      if (t + 2 == nk && has_next) set_src(m1, n1);     // the stream crosses into the next tile
       read_b(sB, 0, fb);                                // phase 0: Q00
       read_a(sA, 0);
       PP_READ_DONE();
@@ -441,13 +457,13 @@ __global__ __launch_bounds__(512, 1) void gemm_8pp_kernel(GemmA a, const bf16* _
       mfma_q(0, 1, fb2);
       PP_MFMA_DONE();
       read_a(sA, 1);                                    // phase 2: Q11 + W of the K-tile two steps ahead
-      if (more2) { dma(2, tm0, tn0, tk, g & 1); dma(3, tm0, tn0, tk, g & 1); }
+      if (more2) { dma(2, tk, g & 1); dma(3, tk, g & 1); }
       PP_READ_DONE();
       mfma_q(1, 1, fb2);
       PP_MFMA_DONE();
       if (more2) {                                      // phase 3: Q10 + its A
-        dma(0, tm0, tn0, tk, g & 1);
-        dma(1, tm0, tn0, tk, g & 1);
+        dma(0, tk, g & 1);
+        dma(1, tk, g & 1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -460,90 +476,86 @@ __global__ __launch_bounds__(512, 1) void gemm_8pp_kernel(GemmA a, const bf16* _
 #undef PP_MFMA_DONE
     if (wm == 0) asm volatile("s_barrier" ::: "memory");   // balance the stagger
 
-    // ---- epilogue through the 32 KiB staging region
+    // ---- epilogue: raw f32 accumulators staged 32 rows at a time through the 32 KiB region; the bias (and
+    // GELU, and the residual) are applied on the store side, where each thread's output columns are the same in
+    // every pass, so the bias is loaded once per tile and no load sits between one pass's stores and the next
+    // (a load there would wait for those stores: vmcnt counts them).  Same f32 arithmetic as epi_value4.
     char* stg = (char*)(smem + PP_STAGE);
     constexpr bool BF16_OUT = KIND == EPI_BF16;
-    if (BF16_OUT) {
+    const int cq = BF16_OUT ? (tid & 31) * 8 : (tid & 63) * 4;      // this thread's first output column
+    f32x4 bias0 = f32x4{0.f, 0.f, 0.f, 0.f}, bias1 = bias0;
+    if (epi.bias) {
+      bias0 = *(const f32x4*)(epi.bias + min(n0 + cq, N - 4));
+      if (BF16_OUT) bias1 = *(const f32x4*)(epi.bias + min(n0 + cq + 4, N - 4));
+    }
+    f32x4 rn[4];                                        // RESID_F32: the next pass's residual chunks
+    auto load_res = [&](int p, f32x4 (&dst)[4]) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {                     // rows [64 p, 64 p + 64): wave group p >> 1, fragments 4 (p & 1) ..
-        if (wm == (p >> 1)) {
-#pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            const int i = (p & 1) * 4 + ii, rl = ii * 16 + fr;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              const int cl = wn * 64 + jj * 16 + 4 * fq;
-              const f32x4 v = epi_value4<KIND>(epi, m0 + wm * 128 + i * 16 + fr, min(n0 + cl, N - 4), acc[i][jj]);
-              bf16x4 o;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-              *(bf16x4*)(stg + rl * 512 + (((cl >> 3) ^ (rl & 15)) << 4) + ((cl >> 2) & 1) * 8) = o;
-            }
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int c = tid + 512 * k, rl = c >> 5, ch = c & 31;
-          const int row = m0 + p * 64 + rl, col0 = n0 + ch * 8;
-          const bf16x8 v = *(const bf16x8*)(stg + rl * 512 + ((ch ^ (rl & 15)) << 4));
-          if (row < M && col0 < N) epi_store8_bf16<KIND>(epi, row, col0, v);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
+      for (int k = 0; k < 4; ++k) {
+        const int row = min(m0 + p * 32 + (tid >> 6) + 8 * k, M - 1), col0 = min(n0 + cq, N - 4);
+        dst[k] = *(const f32x4*)((const float*)epi.out + (long long)row * epi.ldc + col0);
       }
-    } else {
-      f32x4 rn[4];                                      // RESID_F32: residual chunks of the next pass
-      auto load_res = [&](int p, f32x4 (&dst)[4]) {
+    };
+    if (KIND == EPI_RESID_F32) load_res(0, rn);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int c = tid + 512 * k, rl = c >> 6, cc = (c & 63) * 4;
-          const int row = min(m0 + p * 32 + rl, M - 1), col0 = min(n0 + cc, N - 4);
-          dst[k] = *(const f32x4*)((const float*)epi.out + (long long)row * epi.ldc + col0);
-        }
-      };
-      if (KIND == EPI_RESID_F32) load_res(0, rn);
+    for (int p = 0; p < 8; ++p) {                       // rows [32 p, 32 p + 32): wave group p >> 2, fragments 2 (p & 3) ..
+      f32x4 rc[4];
+      if (KIND == EPI_RESID_F32) {
 #pragma unroll
-      for (int p = 0; p < 8; ++p) {                     // rows [32 p, 32 p + 32): wave group p >> 2, fragments 2 (p & 3) ..
-        f32x4 rc[4];
-        if (KIND == EPI_RESID_F32) {
+        for (int k = 0; k < 4; ++k) rc[k] = rn[k];
+        if (p + 1 < 8) load_res(p + 1, rn);
+      }
+      if (wm == (p >> 2)) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) rc[k] = rn[k];
-          if (p + 1 < 8) load_res(p + 1, rn);
-        }
-        if (wm == (p >> 2)) {
+        for (int ii = 0; ii < 2; ++ii) {
+          const int rl = ii * 16 + fr;
 #pragma unroll
-          for (int ii = 0; ii < 2; ++ii) {
-            const int i = (p & 3) * 2 + ii, rl = ii * 16 + fr;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              const int cl = wn * 64 + jj * 16 + 4 * fq;
-              *(f32x4*)(stg + rl * 1024 + (((cl >> 2) ^ (rl & 15)) << 4)) =
-                  epi_value4<KIND>(epi, m0 + wm * 128 + i * 16 + fr, min(n0 + cl, N - 4), acc[i][jj]);
-            }
+          for (int jj = 0; jj < 4; ++jj) {
+            const int cl = wn * 64 + jj * 16 + 4 * fq;
+            *(f32x4*)(stg + rl * 1024 + (((cl >> 2) ^ (rl & 15)) << 4)) = acc[(p & 3) * 2 + ii][jj];
           }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
+      if (BF16_OUT) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int rl = (tid >> 5) + 16 * k, row = m0 + p * 32 + rl, col0 = n0 + cq;
+          const int c4 = cq >> 2;                       // first of the two f32 chunks
+          f32x4 v0 = *(const f32x4*)(stg + rl * 1024 + ((c4 ^ (rl & 15)) << 4)) + bias0;
+          f32x4 v1 = *(const f32x4*)(stg + rl * 1024 + (((c4 + 1) ^ (rl & 15)) << 4)) + bias1;
+          if (epi.act == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v0[e] = gelu_erf(v0[e]); v1[e] = gelu_erf(v1[e]); }
+          }
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { o[e] = f2bf(v0[e]); o[4 + e] = f2bf(v1[e]); }
+          if (row < M && col0 < N) epi_store8_bf16<KIND>(epi, row, col0, o);
+        }
+      } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const int c = tid + 512 * k, rl = c >> 6, ch = c & 63;
-          const int row = m0 + p * 32 + rl, col0 = n0 + ch * 4;
-          const f32x4 v = *(const f32x4*)(stg + rl * 1024 + ((ch ^ (rl & 15)) << 4));
+          const int rl = (tid >> 6) + 8 * k, row = m0 + p * 32 + rl, col0 = n0 + cq;
+          const f32x4 v = *(const f32x4*)(stg + rl * 1024 + (((cq >> 2) ^ (rl & 15)) << 4)) + bias0;
           if (row < M && col0 < N) {
             if (KIND == EPI_RESID_F32) *(f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0) = rc[k] + v;
-            else epi_store4_f32<KIND>(epi, row, col0, v);
+            else *(f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0) = v;
           }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: no vmcnt(0)
       }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
   }
 }
 
-// Process-wide (the GEMM launchers carry no engine): VLOG_AMD_GEMM_PERSIST=0 or wm_set_option("gemm_persistent", 0)
-// restores the one-tile-per-block kernel.  Bit-identical either way.
+// Process-wide (the GEMM launchers carry no engine): VLOG_AMD_GEMM_PERSIST=1 or wm_set_option("gemm_persistent", 1)
+// selects the persistent kernel.  Bit-identical either way.  Off by default: measured equal in bench.py (encoder
+// GEMM 296.9-298.7 vs 296.1-296.2 ms per step) and 3-7 % slower in tools/gemm_bench on the 16-window shapes, so
+// a tile's fixed cost is not its prologue round trip (profiles/ab_r02_persist.txt).
 static int g_gemm_persist = [] {
   const char* e = std::getenv("VLOG_AMD_GEMM_PERSIST");
-  return e ? std::atoi(e) : 1;
+  return e ? std::atoi(e) : 0;
 }();
 static int gemm_8p_persistent() { return g_gemm_persist; }
 void gemm_8p_set_persistent(int on) { g_gemm_persist = on != 0; }
@@ -571,7 +583,7 @@ static int gemm_8p_group() {
 template <int KIND>
 static void run_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st) {
   {
-    constexpr bool PK = KIND == EPI_BF16 || KIND == EPI_RESID_F32 || KIND == EPI_F32 || KIND == EPI_GELU_POS_F32;
+    constexpr bool PK = KIND == EPI_BF16 || KIND == EPI_RESID_F32 || KIND == EPI_F32;
     const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = (N + P8_BN - 1) / P8_BN;
     const int n_tiles = tiles_m * tiles_n, cus = device_cus();
     const bool out_ok = KIND == EPI_BF16 ? (N % 8 == 0 && epi.ldc % 8 == 0 && (epi.rpb == 0 || epi.bstride % 8 == 0))
