@@ -1,16 +1,13 @@
-# A/B of an engine env knob on the bench (no parity / cpu baseline), then the config parity tests.
+# bench.py A/B of env-knob arms (ARMS, ':' joins variables of one arm), then (unless NOFULL) the full GPU suite.
 set -o pipefail
-R=$GRAFT_REPO_ROOT
-cd $R
-mkdir -p gpurun_out
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 TAG=${TAG:-ab}
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-parity --no-cpu-baseline > gpurun_out/bench_${TAG}_a.json 2> gpurun_out/bench_${TAG}_a.err && python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_a.json'));print('A',d['value'],d['stages_s_per_step'],{k:v['ms'] for k,v in d['kernels_one_step'].items()})" &&
-env $KNOB timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-parity --no-cpu-baseline > gpurun_out/bench_${TAG}_b.json 2> gpurun_out/bench_${TAG}_b.err && python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_b.json'));print('B',d['value'],d['stages_s_per_step'],{k:v['ms'] for k,v in d['kernels_one_step'].items()})" || exit $?
-if [ -n "$TESTS" ]; then
-  export VLOG_AMD_PARITY_OUT=$R/gpurun_out/parity_$TAG.jsonl
-  rm -f $VLOG_AMD_PARITY_OUT
-  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v --timeout 400 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
-  rc=$?
-  tail -15 gpurun_out/tests_$TAG.log
-  exit $rc
-fi
+i=0
+for kv in $ARMS; do
+  i=$((i+1))
+  env ${kv//:/ } timeout -k 10 300 python bench.py --no-cpu-baseline --no-parity > gpurun_out/${TAG}_$i.json 2> gpurun_out/${TAG}_$i.err || { tail -20 gpurun_out/${TAG}_$i.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels_one_step']; print(sys.argv[2], d['value'], d['config']['token_crc32'], {n: round(k[n]['ms'],1) for n in k})" gpurun_out/${TAG}_$i.json "$kv"
+done
+[ -n "$NOFULL" ] && exit 0
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1; rc=$?; tail -4 gpurun_out/${TAG}_tests.log; [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/${TAG}_tests.log | head -20; exit $rc; }
+exit 0
