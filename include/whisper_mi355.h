@@ -211,6 +211,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "gemm_persistent" (default 0, process-wide): 1 runs large encoder GEMMs as one persistent block per CU
  *   walking its tiles, the next tile's first K-tiles loaded during the current tile's last K-steps and epilogue
  *   (measured no faster than one block per tile).  Bit-identical.
+ *   "cross_attn_keep" (default 0): the factored cross-attention loads the encoder output of the first that many
+ *   windows with the default cache policy and the rest non-temporally (an Infinity Cache residency experiment;
+ *   measured no gain).  Bit-identical.
  *   "cross_attn_snake" (default 0): odd decoder layers walk the factored cross-attention's items in reverse, so
  *   the encoder output read last by one layer is read first by the next (Infinity Cache reuse).  Bit-identical.
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its

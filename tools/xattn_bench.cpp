@@ -9,7 +9,7 @@
 #include <vector>
 typedef __bf16 bf16;
 void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int,
-                  int, int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t,
+                  int, int, int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t,
                   hipEvent_t);
 void xattn_set_ablation(int);
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
@@ -55,6 +55,7 @@ int main(int argc, char** argv) {
   // XB_SNAKE=1: consecutive launches walk the items in opposite orders (Infinity Cache reuse between launches)
   const int snake = getenv("XB_SNAKE") ? atoi(getenv("XB_SNAKE")) : 0;
   int launch_no = 0;
+  const int keep = getenv("XB_KEEP") ? atoi(getenv("XB_KEEP")) : 0;   // windows loaded with the default policy
   for (int f8 = 0; f8 < 2; ++f8) {
     if (f8_only >= 0 && f8 != f8_only) continue;
     const double bytes = (double)W * T * d * (f8 ? 1 : 2);
@@ -62,7 +63,7 @@ int main(int argc, char** argv) {
       xattn_set_ablation(abl);
       for (int splits : split_list) {
         auto run = [&] {
-          launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, splits, snake ? (launch_no++ & 1) : 0, pu, pml, nullptr,
+          launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, splits, snake ? (launch_no++ & 1) : 0, keep, pu, pml, nullptr,
                        nullptr, 0, nullptr, 0, nullptr, nullptr);
         };
         for (int i = 0; i < 3; ++i) run();

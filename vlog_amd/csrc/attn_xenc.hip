@@ -183,6 +183,7 @@ struct XAttnArgs {
   const int* hyp_slot; const int* row_hyp; const int* done;
   int H, T, d, G, n_mt, splits, n_items, per_xcd;
   int rev;                               // 1: each XCD walks its items in reverse (see launch_xattn)
+  int keep;                              // window groups < keep load E with the default cache policy (else nt)
   long long slab_rows;                   // rows of the whole pass: partial slab stride
   bf16* part_u;                          // [splits][H][d/16][slab_rows][16]   u_s / l_s
   float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
@@ -453,8 +454,12 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   const int mt = item % a.n_mt;
   const int rest = item / a.n_mt;
   const int split = rest % a.splits, grp = rest / a.splits;
-  xattn_segment<QW, NW, DEPTH, F8, ABL, CAP>(a, smem, grp, mt, split, split * n_tiles / a.splits,
-                                        (split + 1) * n_tiles / a.splits);
+  const int tb = split * n_tiles / a.splits, te = (split + 1) * n_tiles / a.splits;
+  // a uniform choice per workgroup between two instantiations (no branch inside the tile loop): the first
+  // `keep` window groups stream E with default-policy loads, which may stay in the Infinity Cache for the next
+  // layer, the rest with non-temporal loads, which should not evict them
+  if (ABL == 0 && grp < a.keep) xattn_segment<QW, NW, DEPTH, F8, 8, CAP>(a, smem, grp, mt, split, tb, te);
+  else xattn_segment<QW, NW, DEPTH, F8, ABL, CAP>(a, smem, grp, mt, split, tb, te);
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -684,7 +689,7 @@ static int g_xattn_abl = [] {            // ablation / load-policy experiments (
 void xattn_set_ablation(int abl) { g_xattn_abl = abl; }
 
 void launch_xattn(const bf16* qp, const void* enc, const float* escale, const int* hyp_slot, const int* row_hyp,
-                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, int rev, bf16* part_u,
+                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, int rev, int keep, bf16* part_u,
                   float* part_ml, float* probs, const int* head_map, int n_align, unsigned long long* stat,
                   hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
@@ -692,7 +697,7 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
   if (splits < 1 || splits > XMAXS || splits > (T + 31) / 32) throw std::runtime_error("xattn: bad key splits");
   XAttnArgs a{};
   a.qp = qp; a.enc = (const bf16*)enc; a.escale = escale; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
-  a.H = H; a.T = T; a.d = d; a.G = group; a.n_mt = (group * H + 31) / 32; a.splits = splits; a.rev = rev;
+  a.H = H; a.T = T; a.d = d; a.G = group; a.n_mt = (group * H + 31) / 32; a.splits = splits; a.rev = rev; a.keep = keep;
   const long long items = (long long)(rows / group) * a.n_mt * splits;
   if (items > (1LL << 30)) throw std::runtime_error("xattn: too many work items");
   a.n_items = (int)items;

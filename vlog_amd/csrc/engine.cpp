@@ -47,7 +47,7 @@ void launch_xpack(const bf16*, bf16*, bf16*, int, int, int, hipStream_t);
 void launch_xq(const bf16*, long long, const CrossFuse&, const bf16*, bf16*, int, int, int, hipStream_t);
 int xattn_splits(int, int, int, int, int);
 void launch_xquant8(const bf16*, long long, int, unsigned char*, float*, hipStream_t);
-void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int, int,
+void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int, int, int,
                   bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, const float*, const int*, const int*, bf16*,
                      long long, int, int, int, int, int, float*, const int*, int, hipStream_t);
@@ -171,6 +171,8 @@ struct wm_engine {
   // holds its encoder output, 3.84 MB for large-v3), 0 = projected cross-KV panels (attn_dec.hip: 245.8 MB
   // per large-v3 window, projected by wm_cross_kv)
   int cross_mode = 1;
+  int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
+                             // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
   DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs (cross_fp8: OCP e4m3 bytes)
   DevBuf xscale;             // cross_fp8: [n_slots][T] f32 per-position scales
@@ -577,7 +579,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     {
       ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
       launch_xattn(qp, e->xenc.p, e->cross_fp8 ? e->xscale.as<float>() : nullptr, e->d_hyp_slot.as<int>(), row_hyp, done, rows, sl.total_rows, cross_group, H, T,
-                   d, splits, e->xsnake ? (l & 1) : 0, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+                   d, splits, e->xsnake ? (l & 1) : 0, e->xkeep, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
     }
     {
       ProfScope ps(e, P_CROSS_COMB, st, 2.0 * rows * d * d, 2.0 * d * d + 2.0 * splits * rows * prow + 2.0 * rows * d);
@@ -1188,6 +1190,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_MODE")) e->cross_mode = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_XSNAKE")) e->xsnake = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_XKEEP")) e->xkeep = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
     try {
       build_layout(e);
@@ -1454,6 +1457,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_attn_blocks") e->cross_cap = (int)std::max<int64_t>(0, value);
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else if (k == "cross_attn_snake") e->xsnake = value != 0;
+    else if (k == "cross_attn_keep") e->xkeep = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
     else if (k == "gemm_persistent") gemm_8p_set_persistent((int)value);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
     else if (k == "cross_fp8") {
