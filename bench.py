@@ -56,8 +56,9 @@ def build_shard(rank: int, W: int):
 
 class Pipeline:
     def __init__(self, eng, tok, dims, rank, world, W, beam, pcm_dev, margin_left, n_total, host_group=None,
-                 words: bool = False):
+                 words: bool = False, check_every: int = 4):
         self.eng, self.tok, self.dims = eng, tok, dims
+        self.check_every = check_every
         self.words = words
         if words:
             # the product's word-timestamp glue (WhisperModel.add_word_timestamps / find_alignment: one batched
@@ -99,7 +100,7 @@ class Pipeline:
         torch.cuda.synchronize(eng.device)
         t2 = time.perf_counter()
         res, steps = eng.generate(list(range(W)), [self.prompt] * W, beam_size=self.beam, suppress_tokens=self.suppress,
-                                  max_length=448, check_every=8)
+                                  max_length=448, check_every=self.check_every)
         t3 = time.perf_counter()
         groups = []
         for w, r in enumerate(res):
@@ -268,6 +269,7 @@ def main():
     ap.add_argument("--beam", type=int, default=1)
     ap.add_argument("--word-timestamps", action="store_true", help="config 5: batched word alignment in every step")
     ap.add_argument("--eot-after", type=int, default=110)
+    ap.add_argument("--check-every", type=int, default=4, help="decode steps between host polls of the live count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: profiles/traffic_r02_f.json, "
                     "or traffic_r02_fp8.json with --cross-fp8)")
@@ -310,7 +312,7 @@ def main():
     eng.reserve(W, W * max(1, args.beam))
     log(f"[rank {rank}] setup {time.perf_counter() - t:.1f} s, engine {eng.device_bytes() / 2**30:.1f} GiB")
     pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total, host_group,
-                    words=args.word_timestamps)
+                    words=args.word_timestamps, check_every=args.check_every)
 
     def barrier():
         torch.cuda.synchronize(eng.device)
