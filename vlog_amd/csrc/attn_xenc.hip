@@ -93,6 +93,16 @@ __global__ void xpack_kernel(const bf16* __restrict__ ckv_w, bf16* __restrict__ 
   }
 }
 
+// XCD-aware flattening of a (gx, gy) grid launched as gx * gy one-dimensional blocks: blocks with consecutive
+// remapped ids (the gx blocks of one y) run on one XCD, so what they share (a head's weight slice) is fetched
+// into that XCD's L2 once instead of by every XCD (speed only: any placement gives the same results).
+__device__ __forceinline__ void xcd_block(int gx, int& bx, int& by) {
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  by = wgid / gx;
+  bx = wgid - by * gx;
+}
+
 // ------------------------------------------------------------------------------------------------------
 struct XQArgs {
   const bf16* q; long long ldq;          // q rows [rows][ldq] (unused when q_part is set)
@@ -103,27 +113,29 @@ struct XQArgs {
   float scale;
 };
 
-// grid (ceil(rows / 32), H, ceil(d / 256)); wave w computes c-tiles 8z + 2w and 8z + 2w + 1 of head y for
-// 32 rows.  D[c][r] = sum_j Wk^T[c][j] q[r][h*64 + j]: A = Wk^T rows (16-B loads), B = q rows.  The block
+// grid ceil(rows / 32) x H x ceil(d / 256) flattened (xcd_block); wave w computes c-tiles 8z + 2w and 8z + 2w + 1
+// of head y for 32 rows.  D[c][r] = sum_j Wk^T[c][j] q[r][h*64 + j]: A = Wk^T rows (16-B loads), B = q rows.  The block
 // first builds its 32 x 64 q tile in LDS: 8 elements per thread, every slab load issued before any add
 // (the slab sum is then one memory round trip, not one per slab), summed in slab order plus the bias as
 // splitk_reduce_kernel does, so the value is bit-identical to the unfused projection's bf16 q.
 __global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 sq[32 * 72];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
-  const int h = blockIdx.y;
-  const int n_ct = a.d / 32;
+  const int n_ct = a.d / 32, gz = (n_ct + 7) / 8;
+  int bx, hz;
+  xcd_block((a.rows + 31) / 32, bx, hz);              // the row tiles of one (head, column group) on one XCD
+  const int h = hz / gz, bz = hz - h * gz;
   // this wave's Wk^T fragments first (independent of q: one memory round trip with the q loads)
   bf16x8 wf[2][4];
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci) {
-    const int ct = min(blockIdx.z * 8 + wv * 2 + ci, n_ct - 1);
+    const int ct = min(bz * 8 + wv * 2 + ci, n_ct - 1);
     const bf16* wr = a.wkt + ((long long)h * a.d + ct * 32 + l32) * 64 + 8 * hh;
 #pragma unroll
     for (int s = 0; s < 4; ++s) wf[ci][s] = *(const bf16x8*)(wr + 16 * s);
   }
   {
-    const int rr = tid >> 3, c8 = (tid & 7) * 8, r = min(blockIdx.x * 32 + rr, a.rows - 1);
+    const int rr = tid >> 3, c8 = (tid & 7) * 8, r = min(bx * 32 + rr, a.rows - 1);
     bf16x8 qv;
     const int col = h * 64 + c8;
     if (a.q_part) {
@@ -151,13 +163,13 @@ __global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
     *(bf16x8*)(sq + rr * 72 + c8) = qv;
   }
   __syncthreads();
-  const int r = blockIdx.x * 32 + l32;
+  const int r = bx * 32 + l32;
   bf16x8 qb[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qb[s] = *(const bf16x8*)(sq + l32 * 72 + 16 * s + 8 * hh);
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci) {
-    const int ct = blockIdx.z * 8 + wv * 2 + ci;
+    const int ct = bz * 8 + wv * 2 + ci;
     if (ct >= n_ct) break;
     f32x16 acc = xzero16();
 #pragma unroll
@@ -472,7 +484,7 @@ struct XCombArgs {
   float* probs; const int* head_map; int n_align;
 };
 
-// grid (ceil(rows / 32), H), 8 waves.  D[r][j] = sum_c u[r][h][c] Wv[h*64 + j][c]: A = merged u rows (built
+// grid ceil(rows / RT) x H flattened (xcd_block), 8 waves.  D[r][j] = sum_c u[r][h][c] Wv[h*64 + j][c]: A = merged u rows (built
 // from the bf16 split partials while loading), B = Wv rows.  Wave w reduces c in [w d/8, (w+1) d/8): its
 // partial and weight loads are issued KB k-steps at a time (one memory round trip per batch, not per
 // k-step).  The merged u is split into bf16 hi + lo parts (two MFMAs), so the V projection sees u to
@@ -486,8 +498,9 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
   __shared__ float sR[8][2][16][64];
   __shared__ float sML[32][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
-  const int h = blockIdx.y;
-  const int r = blockIdx.x * RT + (l32 & (RT - 1));
+  int bx, h;
+  xcd_block((a.rows + RT - 1) / RT, bx, h);
+  const int r = bx * RT + (l32 & (RT - 1));
   const int rc = min(r, a.rows - 1);
   const long long sstride = a.slab_rows * a.H;          // (row, head) pairs per split slab
   float w[MAXS];
@@ -571,7 +584,7 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
     const int j = 32 * jt + (ln & 31);
     const int tr = 8 * (i >> 2) + 4 * (ln >> 5) + (i & 3);
     if (tr >= RT) continue;
-    const int rr = blockIdx.x * RT + tr;
+    const int rr = bx * RT + tr;
     if (rr < a.rows && !(a.done && a.done[a.row_hyp[rr]]))
       a.out[(long long)rr * a.ldo + h * 64 + j] = f2bf(v + a.bv[h * 64 + j]);
   }
@@ -580,7 +593,7 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
     if (hm >= 0) {
       for (int idx = tid; idx < RT * a.T; idx += 512) {
         const int ri = idx / a.T, t = idx - ri * a.T;
-        const int rr = blockIdx.x * RT + ri;
+        const int rr = bx * RT + ri;
         if (rr >= a.rows) continue;
         float* p = a.probs + ((long long)rr * a.n_align + hm) * a.T + t;
         *p = __builtin_amdgcn_exp2f(*p - sML[ri][0]) / sML[ri][1];
@@ -655,7 +668,7 @@ void launch_xq(const bf16* q, long long ldq, const CrossFuse& fz, const bf16* wk
   a.q = q; a.ldq = ldq; a.q_part = fz.q_part; a.q_splits = fz.q_splits; a.q_rows = fz.q_rows; a.q_bias = fz.q_bias;
   a.wkt = wkt; a.qp = qp; a.rows = rows; a.H = H; a.d = d;
   a.scale = 0.125f * 1.4426950408889634f;
-  const dim3 grid((rows + 31) / 32, H, (d / 32 + 7) / 8);
+  const dim3 grid((rows + 31) / 32 * H * ((d / 32 + 7) / 8));   // flattened (row tile, head, column group)
   hipLaunchKernelGGL(xq_kernel, grid, dim3(256), 0, st, a);
   WM_LAUNCH_CHECK("xq_kernel");
 }
@@ -777,7 +790,7 @@ void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long 
     return e ? std::atoi(e) : 0;
   }();
   const int rt = rt_forced == 16 || rt_forced == 32 ? rt_forced : ((rows + 31) / 32 * H >= 256 ? 32 : 16);
-  const dim3 grid((rows + rt - 1) / rt, H);
+  const dim3 grid((rows + rt - 1) / rt * H);           // flattened (row tile, head): xcd_block
 #define XC_RT(KS8_, MS_)                                                                                          \
   if (rt == 16) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 16>), grid, dim3(512), 0, st, a);                  \
   else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 32>), grid, dim3(512), 0, st, a);
