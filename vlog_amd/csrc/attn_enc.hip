@@ -182,15 +182,27 @@ typedef __attribute__((ext_vector_type(2))) int i32x2;
 __device__ __forceinline__ int a2_kslot(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 7)) << 3); }
 __device__ __forceinline__ int a2_vslot(int r, int c) { return r * 64 + ((c ^ (((r >> 1) & 1) << 2)) << 3); }
 
+// Grid: (query tiles x heads x windows) flattened, XCD-aware: the query tiles of one (window, head) get
+// consecutive remapped ids, i.e. one XCD, so that head's K/V (1500 x 64 x 2 x 2 B) is read into that XCD's L2
+// once instead of by every XCD (placement only: results do not depend on it).
 __global__ __launch_bounds__(256, 2) void attn_enc_v2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                             int T, int d, float scale_log2) {
+                                                             int T, int d, float scale_log2, int n_head) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * A2_KT * HD];     // [buf][K | V][64 keys][64]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ql = lane & 31, hh = lane >> 5;
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int nqt = (T + 127) / 128;
+  int qt, h, b;
+  {
+    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    qt = wgid % nqt;
+    const int rest = wgid / nqt;
+    h = rest % n_head;
+    b = rest / n_head;
+  }
   const long long ld = 3LL * d;
   const bf16* base = qkv + (long long)b * T * ld + h * HD;
-  const int q = blockIdx.x * 128 + wv * 32 + ql;
+  const int q = qt * 128 + wv * 32 + ql;
 
   // Q (B operand of S^T): k-step s holds Q[q][16 s + 8 hh + j], pre-scaled
   bf16x8 qf[4];
@@ -353,8 +365,9 @@ void launch_attn_enc(const bf16* qkv, bf16* out, int B, int T, int d, int n_head
     dim3 grid((T + 63) / 64, n_head, B);
     hipLaunchKernelGGL(attn_enc_kernel, grid, dim3(256), 0, st, qkv, out, T, d, scale_log2);
   } else {
-    dim3 grid((T + 127) / 128, n_head, B);
-    hipLaunchKernelGGL(attn_enc_v2_kernel, grid, dim3(256), 0, st, qkv, out, T, d, scale_log2);
+    const long long nblk = (long long)((T + 127) / 128) * n_head * B;
+    if (nblk > (1LL << 31) - 1) throw std::runtime_error("attn_enc: grid too large");
+    hipLaunchKernelGGL(attn_enc_v2_kernel, dim3((unsigned)nblk), dim3(256), 0, st, qkv, out, T, d, scale_log2, n_head);
   }
   WM_LAUNCH_CHECK("attn_enc_kernel");
 }
