@@ -163,6 +163,7 @@ struct wm_engine {
   // preset 0 is round 1's routing.
   int dec_plan[6] = {96, 32, 32, 32, 64, 64};
   int dec_cols[6] = {32, 32, 32, 32, 64, 64};   // ring GEMM output columns per block (32 or 64)
+  int dec_kr[6] = {0, 0, 0, 0, 0, 0};           // ring GEMM K range per block (0: the whole K up to 1280)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
@@ -511,7 +512,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     const int p = plan_of(proj);
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
-    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, K <= 1280 ? K : 1280, st, p, e->dec_cols[proj])) return;
+    const int kr = e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 ? K : 1280);
+    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, e->dec_cols[proj])) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
     launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
@@ -541,7 +543,9 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   CrossFuse fz;
   {
     GemmEpi ep = epi_of(EPI_BF16, q, d, W.cq_b);
-    const int sk = plan_of(DEC_CQ) != -1 ? 1 : skinny_splits(rows, d, d, wsb);
+    const int pcq = plan_of(DEC_CQ);
+    const int sk = pcq == -1 ? skinny_splits(rows, d, d, wsb)
+                             : (pcq > 0 && e->dec_kr[DEC_CQ] > 0 ? (d + e->dec_kr[DEC_CQ] - 1) / e->dec_kr[DEC_CQ] : 1);
     if ((e->cross_fuse & 1) && !(attn && align_map) && sk > 1) {
       ep.defer_combine = 1;
       fz.q_part = ws; fz.q_splits = sk; fz.q_rows = rows; fz.q_bias = W.cq_b;
@@ -1185,6 +1189,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     };
     if (const char* v = std::getenv("VLOG_AMD_DEC_GEMM")) per_proj(v, e->dec_plan);
     if (const char* v = std::getenv("VLOG_AMD_DEC_COLS")) per_proj(v, e->dec_cols);
+    if (const char* v = std::getenv("VLOG_AMD_DEC_KR")) per_proj(v, e->dec_kr);
     if (const char* v = std::getenv("VLOG_AMD_CROSS_BLOCKS")) e->cross_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FUSE")) e->cross_fuse = std::atoi(v) & 3;
     if (const char* v = std::getenv("VLOG_AMD_ENC_CHUNK")) e->enc_chunk = std::max(1, std::atoi(v));
