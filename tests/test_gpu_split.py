@@ -42,6 +42,7 @@ def _run(eng, dims, split, opts=(), **kw):
     eng.set_option("cross_attn_fuse", 1)
     eng.set_option("cross_attn_blocks", 0)
     eng.set_option("cross_attn_snake", 0)
+    eng.set_option("cross_attn_keep", 0)
     eng.set_option("decode_gemm_plan", 1)          # also restores the preset's column widths
     return res, steps
 
@@ -74,7 +75,8 @@ def test_ring_columns_and_snake_order_bit_identical(batch, kw):
     cols32 = tuple(("decode_gemm_cols." + pj, 32) for pj in ("qkv", "fc1", "out"))
     a, sa = _run(eng, dims, 0, opts=rows64 + cols32, **kw)
     b, sb = _run(eng, dims, 0, opts=rows64 + (("decode_gemm_cols.qkv", 64), ("decode_gemm_cols.fc1", 64),
-                                              ("decode_gemm_cols.out", 64), ("cross_attn_snake", 1)), **kw)
+                                              ("decode_gemm_cols.out", 64), ("cross_attn_snake", 1),
+                                              ("cross_attn_keep", W // 2)), **kw)
     _same(a, sa, b, sb)
     assert sum(len(r.tokens) for r in a) > W * 5
 
@@ -96,3 +98,7 @@ def test_unknown_option_raises(batch):
     _, eng = batch
     with pytest.raises(RuntimeError, match="unknown option"):
         eng.set_option("no_such_knob", 1)
+    with pytest.raises(RuntimeError, match="32 or 64"):
+        eng.set_option("decode_gemm_cols.fc1", 48)
+    with pytest.raises(RuntimeError, match="unknown projection"):
+        eng.set_option("decode_gemm_cols.nope", 64)
