@@ -12,6 +12,7 @@
 // fully coalesced 1 KiB per wave load.  Finished hypotheses are skipped (their rows still flow through
 // the weight-bound GEMMs, which read the weights once per step regardless).
 #include "common.h"
+#include <type_traits>
 #include <hip/hip_ext.h>
 #include <algorithm>
 #include <stdexcept>
@@ -424,8 +425,9 @@ static void launch_group(int n_items, int cap, const DecAttnArgs& a, hipStream_t
 // ------------------------------------------------------------------------------------------------------
 // Self-attention, single pass: one WAVE per (row, head), 4 per block, no LDS and no barriers.  A row's
 // keys are positions 0..pos of its hypothesis, key p read from physical slot lin[hyp][p] (beam lineage).
-// Per 64-key chunk each lane fetches one lineage index and the 8 lane groups get theirs by shuffle; every
-// lane then issues the K and V rows of 8 keys (16 x 16 B in flight) before using them.  Online softmax
+// Per 64-key chunk (one 128-key chunk for 65..128 keys) each lane fetches one lineage index per 64 keys and the 8
+// lane groups get theirs by shuffle; every lane then issues the K and V rows of all its keys of the chunk (16 or 32
+// x 16 B in flight) before using them.  Online softmax
 // per lane group, merged by xor-shuffles; lanes 0-7 store the 64 outputs (16 B each).
 __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int n_pairs) {
   const int lane = threadIdx.x & 63;
@@ -449,22 +451,29 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
   float m = -INFINITY, l = 0.f, o[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = 0.f;
-  for (int kb = 0; kb < nk; kb += 64) {
-    const int pl = kb + lane;
-    const int phl = (lrow && pl < nk) ? lrow[pl] : hyp;
-    bf16x8 kr[8], vr[8];
+  // one chunk of 8 U keys: lane group g takes keys kb + 8 u + g, u < U; every K and V row of the chunk is
+  // requested before any is used (2 U x 16 B in flight per lane)
+  auto chunk = [&](auto uc, int kb) {
+    constexpr int U = decltype(uc)::value, NL = U / 8;
+    int phl[NL];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int j = 0; j < NL; ++j) {
+      const int pl = kb + 64 * j + lane;
+      phl[j] = (lrow && pl < nk) ? lrow[pl] : hyp;
+    }
+    bf16x8 kr[U], vr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
       const int p = kb + u * 8 + g;
-      const int ph = __shfl(phl, u * 8 + g, 64);
+      const int ph = __shfl(phl[u >> 3], (u & 7) * 8 + g, 64);
       const int pc = p < nk ? p : 0;
       const long long ro = (long long)ph * hstride + (long long)pc * HD;
       kr[u] = *(const bf16x8*)(K + ro);
       vr[u] = *(const bf16x8*)(V + ro);
     }
-    float sc[8];
+    float sc[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       float d = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) d = fmaf(qf[i], bf2f(kr[u][i]), d);
@@ -475,12 +484,12 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
     }
     float mx = m;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) mx = fmaxf(mx, sc[u]);
+    for (int u = 0; u < U; ++u) mx = fmaxf(mx, sc[u]);
     const float ms = mx == -INFINITY ? 0.f : mx;
     const float corr = exp2f(m - ms);
-    float pu[8], ps = 0.f;
+    float pu[U], ps = 0.f;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       pu[u] = exp2f(sc[u] - ms);
       ps += pu[u];
     }
@@ -489,11 +498,15 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
     for (int i = 0; i < 8; ++i) {
       float x = o[i] * corr;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x = fmaf(pu[u], bf2f(vr[u][i]), x);
+      for (int u = 0; u < U; ++u) x = fmaf(pu[u], bf2f(vr[u][i]), x);
       o[i] = x;
     }
     m = mx;
-  }
+  };
+  // 65..128 keys: one 128-key chunk (one memory round trip instead of two); otherwise 64-key chunks
+  if (nk > 64 && nk <= 128) chunk(std::integral_constant<int, 16>{}, 0);
+  else
+    for (int kb = 0; kb < nk; kb += 64) chunk(std::integral_constant<int, 8>{}, kb);
 #pragma unroll
   for (int off2 = 8; off2 < 64; off2 <<= 1) {
     const float mo = __shfl_xor(m, off2, 64);
