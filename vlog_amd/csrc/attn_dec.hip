@@ -425,7 +425,7 @@ static void launch_group(int n_items, int cap, const DecAttnArgs& a, hipStream_t
 // ------------------------------------------------------------------------------------------------------
 // Self-attention, single pass: one WAVE per (row, head), 4 per block, no LDS and no barriers.  A row's
 // keys are positions 0..pos of its hypothesis, key p read from physical slot lin[hyp][p] (beam lineage).
-// Per 64-key chunk (one 128-key chunk for 65..128 keys) each lane fetches one lineage index per 64 keys and the 8
+// Per chunk (128 keys while more than 64 remain, else 64) each lane fetches one lineage index per 64 keys and the 8
 // lane groups get theirs by shuffle; every lane then issues the K and V rows of all its keys of the chunk (16 or 32
 // x 16 B in flight) before using them.  Online softmax
 // per lane group, merged by xor-shuffles; lanes 0-7 store the 64 outputs (16 B each).
@@ -503,10 +503,16 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
     }
     m = mx;
   };
-  // 65..128 keys: one 128-key chunk (one memory round trip instead of two); otherwise 64-key chunks
-  if (nk > 64 && nk <= 128) chunk(std::integral_constant<int, 16>{}, 0);
-  else
-    for (int kb = 0; kb < nk; kb += 64) chunk(std::integral_constant<int, 8>{}, kb);
+  // 128-key chunks while more than 64 keys remain (one memory round trip per 128 keys), a 64-key chunk for the rest
+  for (int kb = 0; kb < nk;) {
+    if (nk - kb > 64) {
+      chunk(std::integral_constant<int, 16>{}, kb);
+      kb += 128;
+    } else {
+      chunk(std::integral_constant<int, 8>{}, kb);
+      kb += 64;
+    }
+  }
 #pragma unroll
   for (int off2 = 8; off2 < 64; off2 <<= 1) {
     const float mo = __shfl_xor(m, off2, 64);
