@@ -252,6 +252,13 @@ __global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __re
   const bool act = c < np;
   const long long slab2 = ((long long)M * N) >> 1;
   const float2* pr = (const float2*)(part + (long long)r * N) + (act ? c : 0);
+  // every operand this thread needs (residual, bias, LayerNorm affine) is requested with the slabs, so the
+  // kernel pays one memory round trip instead of one before the sums and another after the statistics
+  const int cc = act ? c : 0;
+  float2* xr = (float2*)((float*)epi.out + (long long)r * epi.ldc);
+  const float2 x0 = xr[cc];
+  const float2 bias2 = epi.bias ? ((const float2*)epi.bias)[cc] : make_float2(0.f, 0.f);
+  const float2 gg = ((const float2*)epi.ln_g)[cc], lb = ((const float2*)epi.ln_b)[cc];
   float2 acc = make_float2(0.f, 0.f);
 #pragma unroll 8
   for (int sp = 0; sp < splitk; ++sp) {
@@ -259,15 +266,13 @@ __global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __re
     acc.x += v.x;
     acc.y += v.y;
   }
-  float2* xr = (float2*)((float*)epi.out + (long long)r * epi.ldc);
   float s = 0.f;
   if (act) {
     if (epi.bias) {
-      const float2 bb = ((const float2*)epi.bias)[c];
-      acc.x += bb.x;
-      acc.y += bb.y;
+      acc.x += bias2.x;
+      acc.y += bias2.y;
     }
-    float2 xv = xr[c];
+    float2 xv = x0;
     xv.x += acc.x;
     xv.y += acc.y;
     xr[c] = xv;
@@ -292,10 +297,9 @@ __global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __re
   for (int i = 0; i < nw; ++i) qt += red[1][i];
   const float rstd = rsqrtf(qt / (float)N + 1e-5f);
   if (act) {
-    const float2 gg = ((const float2*)epi.ln_g)[c], bb = ((const float2*)epi.ln_b)[c];
     bf16x2 o;
-    o[0] = f2bf((acc.x - mean) * rstd * gg.x + bb.x);
-    o[1] = f2bf((acc.y - mean) * rstd * gg.y + bb.y);
+    o[0] = f2bf((acc.x - mean) * rstd * gg.x + lb.x);
+    o[1] = f2bf((acc.y - mean) * rstd * gg.y + lb.y);
     ((bf16x2*)(epi.ln_out + (long long)r * epi.ln_ld))[c] = o;
   }
 }
