@@ -494,7 +494,7 @@ struct XCombArgs {
 // (a block's partial bytes halve; the Wv_h panel is the same).
 template <int KS8, int MAXS, int RT = 32>
 __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
-  constexpr int KB = (16 / MAXS) < KS8 ? (16 / MAXS) : KS8;   // k-steps per load batch (<= 16 partial loads)
+  constexpr int KB = (20 / MAXS) < KS8 ? (20 / MAXS) : KS8;   // k-steps per load batch (<= 20 partial loads)
   __shared__ float sR[8][2][16][64];
   __shared__ float sML[32][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
