@@ -78,6 +78,8 @@ class Pipeline:
         self.prompt = [st.sot, st.lang_token("en"), st.transcribe]
         self.suppress = list(tok.suppressed_tokens([-1]))
         self.stage = {}
+        self.solo = False          # True: this rank steps alone (no cross-rank exchange)
+        self.last_gmax = None
 
     def step(self):
         eng, W, d = self.eng, self.W, self.dims
@@ -85,13 +87,18 @@ class Pipeline:
         frame0 = self.rank * W * 3000
         mel, gmax = eng.logmel(self.pcm_dev, n_samples=self.n_total, pcm_offset=frame0 * 160 - self.margin_left,
                                frame0=frame0, n_frames=W * 3000)
-        if self.world > 1:
+        if self.world > 1 and self.solo:
+            # a step on one rank alone (the untimed parity leg): the other ranks are not in the exchange, so
+            # reuse the whole-file max of the last exchanged step (same PCM, same value)
+            eng.logmel_finalize(mel, gmax, self.last_gmax)
+        elif self.world > 1:
             # faster-whisper's clamp uses the WHOLE file's log-mel max: the one cross-shard value, exchanged
             # as a host float over a gloo group (no RCCL collective on the data path)
             import torch.distributed as dist
             g = torch.tensor([eng.gmax_value(gmax)], dtype=torch.float32)
             dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.host_group)
-            eng.logmel_finalize(mel, gmax, float(g[0]))
+            self.last_gmax = float(g[0])
+            eng.logmel_finalize(mel, gmax, self.last_gmax)
         else:
             eng.logmel_finalize(mel, gmax)          # single shard: the clamp reads the max on the device
         t1 = time.perf_counter()
@@ -284,11 +291,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VLOG_AMD_BENCH_SHARE_GPU=1 + VLOG_AMD_BENCH_BACKEND=gloo: a rehearsal of the N > 1 path with every rank on
+    # the visible GPUs round-robin (RCCL refuses two ranks on one device; no collective is on the data path)
+    if os.environ.get("VLOG_AMD_BENCH_SHARE_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     host_group = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("VLOG_AMD_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         host_group = dist.new_group(backend="gloo")      # host scalars (log-mel max, timing): no RCCL on the data path
 
     dims = model_dims(args.model)
@@ -358,6 +373,7 @@ def main():
     if rank == 0 and not args.no_parity and sd is not None and args.beam == 1:
         from tests.parity_util import sample_indices
         pipe.keep_windows = tuple(sample_indices(W, args.parity_windows))
+        pipe.solo = True                                        # rank 0 alone: no exchange with the other ranks
         pipe.step()                                             # untimed: keeps the sampled windows' encoder output
         try:
             parity = parity_sample(dims, sd, pipe, fp8_cross=args.cross_fp8)
