@@ -90,6 +90,8 @@ class Pipeline:
         if self.world > 1 and self.solo:
             # a step on one rank alone (the untimed parity leg): the other ranks are not in the exchange, so
             # reuse the whole-file max of the last exchanged step (same PCM, same value)
+            if self.last_gmax is None:
+                raise RuntimeError("solo step before any exchanged step: no whole-file log-mel max to reuse")
             eng.logmel_finalize(mel, gmax, self.last_gmax)
         elif self.world > 1:
             # faster-whisper's clamp uses the WHOLE file's log-mel max: the one cross-shard value, exchanged
@@ -330,10 +332,12 @@ def main():
                     words=args.word_timestamps, check_every=args.check_every)
 
     def barrier():
+        # device drained, then a host-side rendezvous over the gloo group: no RCCL call anywhere in the timed
+        # region
         torch.cuda.synchronize(eng.device)
         if world > 1:
             import torch.distributed as dist
-            dist.barrier()
+            dist.barrier(group=host_group)
 
     for _ in range(args.warmup):
         pipe.step()
@@ -404,6 +408,10 @@ def main():
                    "parallelism": f"window-shard x{world}", "weights": f"synthetic seed 0, eot_after={args.eot_after}"},
         "stages_s_per_step": {k: round(v / args.steps, 4) for k, v in stage_timed.items()},
     }
+    if os.environ.get("VLOG_AMD_BENCH_SHARE_GPU") == "1":
+        # a rehearsal of the N > 1 path with several ranks on one device: NOT a scaling result
+        out["config"]["gpus_shared"] = True
+        out["config"]["physical_gpus"] = torch.cuda.device_count()
     if prof:
         kern = {}
         for k, v in breakdown.items():

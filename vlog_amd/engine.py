@@ -101,6 +101,7 @@ class GpuEngine:
     def __init__(self, dims: ModelDims, state_dict: Dict[str, torch.Tensor], device_index: int = 0):
         self.lib = _capi.load()
         self.dims = dims
+        self._opts: Dict[str, int] = {}
         self.device = torch.device("cuda", device_index)
         st = dims.specials
         cd = _capi.ModelDimsC(dims.n_mels, dims.n_state, dims.n_head, dims.n_enc_layer, dims.n_dec_layer,
@@ -179,6 +180,11 @@ class GpuEngine:
     def set_option(self, key: str, value: int) -> None:
         """Engine scheduling knob (wm_set_option), e.g. set_option("decode_split", 0)."""
         _capi.check(self.lib.wm_set_option(self.h, key.encode(), int(value)), "wm_set_option")
+        self._opts[key] = int(value)
+
+    def option(self, key: str, default: Optional[int] = None) -> Optional[int]:
+        """The last value set through set_option (None / default when never set: the engine default)."""
+        return self._opts.get(key, default)
 
     def device_bytes(self) -> int:
         return int(self.lib.wm_device_bytes(self.h))

@@ -204,9 +204,11 @@ class WhisperModel:
         self.max_length = MAX_LENGTH
 
     def _pipeline(self) -> "BatchedInferencePipeline":
-        if self._batched is None:
-            self._batched = BatchedInferencePipeline(self, max_batch_windows=int(os.environ.get("VLOG_AMD_BATCH_WINDOWS", "150")))
-        return self._batched
+        with self._lock:                      # created once even when several worker threads race here
+            if self._batched is None:
+                self._batched = BatchedInferencePipeline(
+                    self, max_batch_windows=int(os.environ.get("VLOG_AMD_BATCH_WINDOWS", "150")))
+            return self._batched
 
     @property
     def is_multilingual(self) -> bool:
@@ -656,7 +658,6 @@ class BatchedInferencePipeline:
     def __init__(self, model: WhisperModel, max_batch_windows: int = 150):
         self.model = model
         self.max_batch_windows = max_batch_windows
-        self._last_speech_by_file: dict = {}
 
     # -- windows of the whole-file feature matrix
     @staticmethod
@@ -687,10 +688,15 @@ class BatchedInferencePipeline:
     def decode_windows(self, features: torch.Tensor, windows: Sequence[Tuple[int, int]], time_offsets: Sequence[float],
                        tokenizer: Tokenizer, options: TranscriptionOptions, seed: int = 0,
                        files: Optional[Sequence[int]] = None,
-                       seek_bases: Optional[Sequence[int]] = None) -> List[WindowResult]:
+                       seek_bases: Optional[Sequence[int]] = None,
+                       last_speech: Optional[dict] = None) -> List[WindowResult]:
         """files: the source file of each window when windows of several files share batches (transcribe_many):
         word timestamps then keep one last-speech time per file.  seek_bases: frame offset of each window's file
-        inside `features` (its segments and word timestamps are reported relative to the file)."""
+        inside `features` (its segments and word timestamps are reported relative to the file).  last_speech:
+        the caller's per-file last-speech times (word-timestamp heuristics); owned by ONE transcribe call, so
+        threads sharing this pipeline never see each other's state."""
+        if last_speech is None:
+            last_speech = {}
         m = self.model
         eng = m.engine
         st = m.dims.specials
@@ -701,14 +707,29 @@ class BatchedInferencePipeline:
             prompt = [tokenizer.sot_prev] + ip[-(m.max_length // 2 - 1):] + prompt
         max_length = min(m.max_length, len(prompt) + options.max_new_tokens) if options.max_new_tokens else m.max_length
         mit = int(round(options.max_initial_timestamp / m.time_precision))
-        out: List[WindowResult] = []
-        B = self.max_batch_windows
         per = max(options.beam_size, options.best_of, 1)
         # cross-attention form per batch: the factored form (attention over the encoder output) reads half the
         # bytes per window and wins for one row per window; with beam / best-of groups the projected K/V form
         # wins (large-v3, 150 windows, beam 5 + words: 1474 vs 1237 RTFx) because every group's rows share one
         # K/V stream there, while the factored kernel re-reads E per 32 (row, head) pairs
-        auto_form = os.environ.get("VLOG_AMD_CROSS_AUTO", "1") != "0"
+        # (opt-in fp8 cross memory is a factored-form mode: the automatic switch never overrides it)
+        auto_form = os.environ.get("VLOG_AMD_CROSS_AUTO", "1") != "0" and not eng.option("cross_fp8", 0)
+        prev_form = eng.option("cross_mode")
+        try:
+            return self._decode_batches(features, windows, time_offsets, tokenizer, options, seed, files, seek_bases,
+                                        last_speech, prompt, max_length, mit, per, auto_form)
+        finally:
+            if auto_form:                      # leave the engine in the form the caller had configured
+                with m._lock:
+                    eng.set_option("cross_mode", 1 if prev_form is None else prev_form)
+
+    def _decode_batches(self, features, windows, time_offsets, tokenizer, options, seed, files, seek_bases,
+                        last_speech, prompt, max_length, mit, per, auto_form) -> List[WindowResult]:
+        m = self.model
+        eng = m.engine
+        st = m.dims.specials
+        out: List[WindowResult] = []
+        B = self.max_batch_windows
         for b0 in range(0, len(windows), B):
             wins = list(windows[b0: b0 + B])
             with m._lock:
@@ -763,10 +784,10 @@ class BatchedInferencePipeline:
                     for f in sorted(set(fid)):
                         idx = [i for i, wr in enumerate(batch) if wr.segments and fid[i] == f]
                         if idx:
-                            self._last_speech_by_file[f] = m.add_word_timestamps(
+                            last_speech[f] = m.add_word_timestamps(
                                 [batch[i].segments for i in idx], tokenizer, [batch[i].size for i in idx],
                                 options.prepend_punctuations, options.append_punctuations,
-                                self._last_speech_by_file.get(f, 0.0), slots=idx)
+                                last_speech.get(f, 0.0), slots=idx)
                 out.extend(batch)
         return out
 
@@ -816,8 +837,7 @@ class BatchedInferencePipeline:
             append_punctuations=append_punctuations, max_new_tokens=max_new_tokens, clip_timestamps=clip_timestamps)
         windows = prep["windows"]
         offsets = [s * HOP_LENGTH / SAMPLE_RATE for s, _ in windows]
-        self._last_speech_by_file = {}
-        results = self.decode_windows(prep["features"], windows, offsets, tokenizer, options)
+        results = self.decode_windows(prep["features"], windows, offsets, tokenizer, options, last_speech={})
         return self._segments(prep["features"], results, tokenizer, options), self._info(prep, options)
 
     def transcribe_many(self, audios: Sequence[Union[str, BinaryIO, np.ndarray]],
@@ -838,7 +858,7 @@ class BatchedInferencePipeline:
         preps = [self._prepare(a, l, vad_filter, vad_parameters, language_detection_segments,
                                language_detection_threshold) for a, l in zip(audios, langs)]
         out: List[Optional[tuple]] = [None] * n
-        self._last_speech_by_file = {}
+        last_speech: dict = {}
         for lang in sorted({p["language"] for p in preps}):
             files = [i for i, p in enumerate(preps) if p["language"] == lang]
             tokenizer = self.model.tokenizer(task=task, language=lang)
@@ -854,7 +874,7 @@ class BatchedInferencePipeline:
                     fids.append(i)
                 base += preps[i]["features"].shape[1]
             results = self.decode_windows(feats, windows, offsets, tokenizer, options, files=fids,
-                                          seek_bases=[bases[f] for f in fids])
+                                          seek_bases=[bases[f] for f in fids], last_speech=last_speech)
             for i in files:
                 mine = [wr for wr, f in zip(results, fids) if f == i]
                 out[i] = (list(self._segments(None, mine, tokenizer, options)), self._info(preps[i], options))
