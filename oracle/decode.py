@@ -30,10 +30,14 @@ NEG_INF = -np.inf
 
 
 def log_softmax(x: np.ndarray) -> np.ndarray:
+    """log-softmax over the last axis; a fully masked row (all -inf) stays all -inf (never NaN)."""
     x = np.asarray(x, dtype=np.float64)
     m = np.max(x, axis=-1, keepdims=True)
-    m = np.where(np.isfinite(m), m, 0.0)
-    return x - m - np.log(np.sum(np.exp(x - m), axis=-1, keepdims=True))
+    live = np.isfinite(m)
+    m = np.where(live, m, 0.0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        out = x - m - np.log(np.sum(np.exp(x - m), axis=-1, keepdims=True))
+    return np.where(live, out, -np.inf)
 
 
 def apply_rules(logits: np.ndarray, sampled: Sequence[int], st, suppress_tokens: Sequence[int],

@@ -12,7 +12,7 @@ from __future__ import annotations
 import json
 import os
 from dataclasses import asdict, dataclass
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -112,6 +112,9 @@ def window_parity(orc, enc_window: np.ndarray, prompt, res, st, opt: GenerateOpt
         ns = float(np.exp(log_softmax(logits[0, list(prompt).index(st.sot)]))[st.no_speech])
     score = cum / (max(len(tokens), 1) ** opt.length_penalty)
     margins = np.array(margins)
+    # fully masked rows are -inf (oracle.decode.log_softmax), never NaN: a NaN here is a checker bug, and
+    # Python's min() would silently skip it
+    assert not np.isnan(margins).any() and not np.isnan(np.asarray(tie_margins, dtype=np.float64)).any(), margins
     k = int(np.argmin(tie_margins)) if tie_margins else -1
     return WindowParity(window, len(tokens), bool(np.all(margins >= 0.0)), float(margins.min()) if margins.size else 0.0,
                         float(res.score), score, float(res.no_speech_prob), ns,
@@ -139,3 +142,99 @@ def sample_indices(n: int, k: int) -> List[int]:
     if k >= n:
         return list(range(n))
     return sorted({int(round(i * (n - 1) / (k - 1))) for i in range(k)})
+
+
+# ------------------------------------------------------------------------------------------------ north_star gates
+GATE_IDENTICAL = 0.99      # greedy token sequences identical on >= 99 % of windows
+GATE_WER = 0.003           # WER delta <= 0.3 % absolute
+GATE_DT = 0.02             # segment start / end within one timestamp token (20 ms)
+
+
+def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists: Sequence[Sequence[int]],
+                        ended: Sequence[bool], st, opt: GenerateOptions):
+    """Several windows in ONE oracle decoder pass (sequences padded with <|endoftext|>: the mask is causal, so
+    padding never changes an earlier position).  -> per window: (margins [steps], no_speech_prob) with
+    margin = logprob of the GPU token minus the best logprob among the OTHER tokens (> 0: the oracle's argmax)."""
+    cross = orc.cross_kv(enc)
+    L = max(len(t) for t in token_lists)
+    toks = np.full((len(token_lists), len(prompt) + L), st.eot, dtype=np.int64)
+    for i, t in enumerate(token_lists):
+        toks[i, :len(prompt)] = prompt
+        toks[i, len(prompt):len(prompt) + len(t)] = t
+    logits, _ = orc.decode(toks, cross)
+    P = len(prompt)
+    out = []
+    for i, t in enumerate(token_lists):
+        seq = list(t) + ([st.eot] if ended[i] else [])
+        ms = np.empty(len(seq))
+        for k, tok in enumerate(seq):
+            lp = log_softmax(apply_rules(logits[i, P - 1 + k], list(t[:k]), st, opt.suppress_tokens, opt.suppress_blank,
+                                         opt.max_initial_timestamp_index, opt.with_timestamps))
+            chosen = lp[tok]
+            lp[tok] = -np.inf
+            ms[k] = chosen - np.max(lp)
+        assert not np.isnan(ms).any()
+        ns = 0.0
+        if st.sot in prompt:
+            ns = float(np.exp(log_softmax(logits[i, list(prompt).index(st.sot)]))[st.no_speech])
+        out.append((ms, ns))
+    return out
+
+
+def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateOptions, tokenizer,
+                 windows: Optional[Sequence[int]] = None, chunk: int = 8, time_offset=lambda w: 0.0) -> dict:
+    """The north_star parity gates over every window (or `windows`): each GPU token sequence is teacher-forced
+    through the oracle (identical = the GPU token is the oracle's argmax at every step, so the oracle's greedy
+    search produces exactly that sequence); windows that are not identical are re-decoded by the oracle's own
+    greedy search.  WER delta = WER of the GPU transcript against the oracle transcript (per-window edit
+    distances summed); segment times compared segment by segment (start/end within 20 ms).
+    enc_of(list of window ids) -> float32 [n, 1500, d] (the GPU's encoder output: parity at the decoder)."""
+    from vlog_amd.metrics import edit_distance, normalize
+    from vlog_amd.segments import split_segments_by_timestamps
+    from oracle.decode import generate_one
+
+    ws = list(range(len(results))) if windows is None else list(windows)
+    ident, margins, ns_diff, non_ident = [], [], 0.0, []
+    oracle_tokens = {}
+    for c0 in range(0, len(ws), chunk):
+        cw = ws[c0:c0 + chunk]
+        enc = enc_of(cw)
+        toks = [list(results[w].tokens) for w in cw]
+        ended = [len(prompt) + len(t) < opt.max_length for t in toks]
+        for j, (w, (ms, ns)) in enumerate(zip(cw, teacher_force_batch(orc, enc, prompt, toks, ended, st, opt))):
+            same = bool(np.all(ms > 0.0))
+            ident.append(same)
+            ns_diff = max(ns_diff, abs(ns - float(results[w].no_speech_prob)))
+            if same:
+                oracle_tokens[w] = toks[j]
+                margins.append(float(np.min(ms)) if ms.size else 0.0)
+            else:
+                non_ident.append(w)
+                r = generate_one(orc, orc.cross_kv(enc[j:j + 1]), prompt, st, opt)
+                oracle_tokens[w] = list(r.tokens)
+    errs, n_ref, dt, seg_mismatch = 0, 0, 0.0, 0
+    for w in ws:
+        ref, hyp = normalize(tokenizer.decode(oracle_tokens[w])), normalize(tokenizer.decode(results[w].tokens))
+        errs += edit_distance(ref, hyp)
+        n_ref += len(ref)
+        a = split_segments_by_timestamps(results[w].tokens, st.timestamp_begin, time_offset(w), 3000, 30.0, 0)[0]
+        b = split_segments_by_timestamps(oracle_tokens[w], st.timestamp_begin, time_offset(w), 3000, 30.0, 0)[0]
+        if len(a) != len(b):
+            seg_mismatch += 1
+            continue
+        for x, y in zip(a, b):
+            dt = max(dt, abs(x["start"] - y["start"]), abs(x["end"] - y["end"]))
+    n = len(ws)
+    return {"n": n, "identical": int(sum(ident)), "identical_frac": round(sum(ident) / max(n, 1), 5),
+            "wer_delta": round(errs / max(n_ref, 1), 6), "segment_max_dt_s": round(dt, 4),
+            "segment_count_mismatch": seg_mismatch, "max_no_speech_diff": ns_diff,
+            "min_margin_identical_nats": round(min(margins), 3) if margins else None,
+            "non_identical_windows": non_ident,
+            "gates": {"identical_frac": GATE_IDENTICAL, "wer_delta": GATE_WER, "segment_dt_s": GATE_DT}}
+
+
+def assert_gates(g: dict) -> None:
+    assert g["identical_frac"] >= GATE_IDENTICAL, g
+    assert g["wer_delta"] <= GATE_WER, g
+    assert g["segment_max_dt_s"] <= GATE_DT + 1e-9, g
+    assert g["segment_count_mismatch"] <= (1.0 - GATE_IDENTICAL) * g["n"], g

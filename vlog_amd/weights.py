@@ -8,8 +8,9 @@ downloading from the HF Hub (`worker/transcription.py:81-85`).  This engine neve
   * a local CTranslate2 directory (`model.bin`, the layout a faster-whisper deployment uses) -> its weights,
     dequantised to float32 (vlog_amd/ct2.py);
   * a name with `VLOG_AMD_MODEL_DIR_<name>` (or `VLOG_AMD_MODEL_ROOT/<name>`) set -> that directory;
-  * `"synthetic:<name>[:seed]"` -> random-init weights of that architecture (there are no real
-    checkpoints in this environment; BASELINE.md "Synthetic audio");
+  * `"synthetic:<name>[:seed][:margin]"` -> random-init weights of that architecture (there are no real
+    checkpoints in this environment; BASELINE.md "Synthetic audio"); `:margin` adds the decisive planted
+    decoder program (plant_margin) used for the token-identity / WER / timestamp gates;
 
 and raises a ValueError otherwise.
 
@@ -24,8 +25,10 @@ from __future__ import annotations
 
 import hashlib
 import json
+import math
 import os
-from typing import Dict, Optional, Tuple
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -81,9 +84,10 @@ def weight_shapes(dims: ModelDims) -> Dict[str, Tuple[int, ...]]:
 
 
 def synthetic_state_dict(dims: ModelDims, seed: int = 0, eot_after: Optional[int] = None,
-                         std: float = 0.02) -> Dict[str, torch.Tensor]:
+                         std: float = 0.02, plant: Optional[str] = None) -> Dict[str, torch.Tensor]:
     """Seeded random-init weights (float32, CPU), HF naming.  Per-tensor generators make any subset
-    reproducible on its own."""
+    reproducible on its own.  plant="margin": the decisive planted program of plant_margin (eot_after is
+    ignored: the script ends the window)."""
     sd: Dict[str, torch.Tensor] = {}
     for name, shape in weight_shapes(dims).items():
         g = _gen(seed, name)
@@ -96,7 +100,11 @@ def synthetic_state_dict(dims: ModelDims, seed: int = 0, eot_after: Optional[int
         else:
             t = std * torch.randn(shape, generator=g)
         sd[name] = t.float()
-    if eot_after is not None:
+    if plant == "margin":
+        plant_margin(sd, dims, seed)
+    elif plant is not None:
+        raise ValueError(f"unknown plant {plant!r}")
+    elif eot_after is not None:
         plant_eot(sd, dims, eot_after, seed)
     return sd
 
@@ -135,6 +143,246 @@ def plant_eot(sd: Dict[str, torch.Tensor], dims: ModelDims, eot_after: int, seed
     slope = EOT_KAPPA * _resid_std(dims.n_dec_layer) / (c_e * float(eot_after))
     pos += slope * torch.arange(pos.shape[0], dtype=torch.float32)[:, None] * u[None, :]
     sd["model.decoder.embed_tokens.weight"][dims.specials.eot] = c_e * u
+
+
+# ----------------------------------------------------------------------------- margin-planted synthetic model
+# Per-window statistics of the seeded speech-like corpus (vlog_amd.audio.speech_like, 64 clips, normalised log-mel
+# as the encoder sees it): for each bit feature, the median over windows of the window-mean projection.  Feature 0
+# is the mean over all mel bins; features 1.. are zero-sum random projections (seed 1234, normalised to unit L1).
+# Recomputed by tools/calibrate_margin.py; only the centring of the bits depends on them.
+_BIT_MEDIANS = {80: (-0.2237, 0.0275, 0.0225, 0.0088, 0.0052, -0.0086),
+                128: (-0.2134, 0.0053, -0.0107, 0.0021, 0.0039, -0.0023)}
+_BIT_SPREADS = {80: (0.0546, 0.0038, 0.0035, 0.0014, 0.0013, 0.0017),
+                128: (0.0472, 0.0013, 0.0020, 0.0014, 0.0011, 0.0013)}
+N_BITS = 6
+
+
+def bit_projections(n_mels: int) -> np.ndarray:
+    """[n_mels, N_BITS] mel-bin weights of the bit features (see _BIT_MEDIANS)."""
+    rng = np.random.default_rng(1234)
+    p = rng.standard_normal((n_mels, N_BITS))
+    p -= p.mean(0)
+    p /= np.abs(p).sum(0)
+    p[:, 0] = 1.0 / n_mels
+    return p
+
+
+@dataclass
+class MarginPlan:
+    """The planted decoder program.  slots[k] = tokens of script slot k (one token, or a +/- pair chosen by
+    bits[k]); kinds[k] in {"text", "ts", "ts_final"}."""
+    slots: List[Tuple[int, ...]]
+    kinds: List[str]
+    bits: List[Optional[int]]
+    first_key: Tuple[int, ...]          # prompt tokens whose unit emits slot 0 (the first timestamp)
+
+
+def margin_plan(dims: ModelDims, seed: int = 0, n_segments: int = 8) -> MarginPlan:
+    st = dims.specials
+    rng = np.random.default_rng(int.from_bytes(hashlib.sha256(f"{seed}:margin_plan".encode()).digest()[:8], "little"))
+    text_ids = rng.choice(np.arange(1000, st.eot - 1000), size=400, replace=False).tolist()
+    slots: List[Tuple[int, ...]] = [(st.timestamp_begin,)]
+    kinds, bits = ["ts"], [None]
+    span = 28.0 / n_segments
+    bit = 0
+    for m in range(n_segments):
+        n = int(rng.integers(10, 15))
+        branch_at = set(rng.choice(np.arange(1, n - 1), size=2, replace=False).tolist())
+        for j in range(n):
+            if j in branch_at and j - 1 not in branch_at:
+                slots.append((text_ids.pop(), text_ids.pop()))
+                bits.append(bit % N_BITS)
+                bit += 1
+            else:
+                slots.append((text_ids.pop(),))
+                bits.append(None)
+            kinds.append("text")
+        a = int(round((m + 1) * span / 0.02))
+        if m == n_segments - 1:
+            slots.append((st.timestamp_begin + a,))
+            kinds.append("ts_final")
+            bits.append(None)
+        elif m % 2 == 1:                                 # a segment boundary that moves with the audio
+            slots.append((st.timestamp_begin + a, st.timestamp_begin + a + 8))
+            kinds.append("ts")
+            bits.append(bit % N_BITS)
+            bit += 1
+        else:
+            slots.append((st.timestamp_begin + a,))
+            kinds.append("ts")
+            bits.append(None)
+    first_key = (st.transcribe,) if dims.multilingual else (st.sot,)
+    return MarginPlan(slots, kinds, bits, first_key)
+
+
+def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) -> MarginPlan:
+    """Plant a decisive, audio-dependent decoder program into seeded random weights (test model for the
+    north_star token-identity / WER / timestamp gates).
+
+    Random-init Whisper weights give near-tied logits (top-1 vs top-2 and the timestamp-forcing gap sit within
+    bf16 noise), so token identity between two correct implementations is a coin toss.  A trained model is
+    decisive; this plants that property while keeping every random weight elsewhere:
+
+    * decoder layer 0's MLP holds a successor table: hidden unit k fires on script slot k's token direction
+      (fc1 row = that direction, bias = threshold) and writes the next slot's direction (fc2 column), so the
+      next token wins by thousands of nats over the input token and every random contribution;
+    * timestamps: a timestamp slot's unit writes both its own direction (the repeated timestamp of a pair;
+      the rules mask text after the first) and the next text slot's (the rules mask timestamps after the
+      second); the last one writes <|endoftext|>;
+    * audio dependence: N_BITS window-level bits.  The conv stem computes mel-bin projections (centred on the
+      corpus median); one uniform-attention head of encoder layer 0 averages them over the window into
+      channels no other layer writes, so the encoder output carries each window's bit value with an exact sign
+      in bf16 and in fp8; one uniform head of decoder layer 0's cross-attention reads them and writes them along
+      a bit direction; a branch slot's two tokens differ by +-alpha times that direction, so the bit's sign
+      picks the token (and segment boundaries move with it).
+    The encoder channel trick: bit channel m and its reference m' receive identical (zero) writes from every
+    random layer and share LayerNorm affines, so E[m] - E[m'] is the planted value alone."""
+    d, H = dims.n_state, dims.n_head
+    hd = d // H
+    st = dims.specials
+    plan = margin_plan(dims, seed)
+    g = _gen(seed, "plant_margin")
+    rng = np.random.default_rng(int.from_bytes(hashlib.sha256(f"{seed}:plant_margin".encode()).digest()[:8], "little"))
+
+    # ---- encoder: stem bit features, averaging head, protected channels
+    nb = N_BITS
+    ch = rng.choice(d, size=6 * nb, replace=False)
+    s_ch, s_ref, m_ch, m_ref, c_ch, c_ref = (ch[i * nb:(i + 1) * nb] for i in range(6))
+    P = torch.from_numpy(bit_projections(dims.n_mels)).float()          # [n_mels, nb]
+    med = _BIT_MEDIANS.get(dims.n_mels, (0.0,) * nb)
+    spread = _BIT_SPREADS.get(dims.n_mels, (0.01,) * nb)
+    b1 = 3.0
+    c1w, c1b = sd["model.encoder.conv1.weight"], sd["model.encoder.conv1.bias"]       # [d, n_mels, 3]
+    c2w, c2b = sd["model.encoder.conv2.weight"], sd["model.encoder.conv2.bias"]       # [d, d, 3]
+    gelu_b1 = float(0.5 * b1 * (1.0 + math.erf(b1 / math.sqrt(2.0))))
+    for j in range(nb):
+        for c in (s_ch[j], s_ref[j], m_ch[j], m_ref[j], c_ch[j], c_ref[j]):
+            c1w[c] = 0.0; c1b[c] = 0.0; c2w[c] = 0.0; c2b[c] = 0.0
+        c1w[s_ch[j], :, 1] = P[:, j]
+        c1b[s_ch[j]] = b1 - float(med[j])
+        c1b[s_ref[j]] = b1
+        c2w[s_ch[j], s_ch[j], 1] = 1.0                   # GELU(y + b1) - GELU(b1) + b1 through the second GELU
+        c2w[s_ref[j], s_ref[j], 1] = 1.0
+        c2b[s_ch[j]] = b1 - gelu_b1
+        c2b[s_ref[j]] = b1 - gelu_b1
+    pos = sd["model.encoder.embed_positions.weight"]
+    pos[:, torch.as_tensor(ch)] = 0.0
+    # layer 0, head h_e: uniform attention (q = 0) averaging (LN[s] - LN[s']) into channel m
+    h_e = 0
+    p0 = "model.encoder.layers.0.self_attn."
+    sl = slice(h_e * hd, (h_e + 1) * hd)
+    sd[p0 + "q_proj.weight"][sl] = 0.0
+    sd[p0 + "q_proj.bias"][sl] = 0.0
+    sd[p0 + "v_proj.weight"][sl] = 0.0
+    sd[p0 + "v_proj.bias"][sl] = 0.0
+    sd[p0 + "out_proj.weight"][:, sl] = 0.0
+    s_enc = _resid_std(dims.n_enc_layer)
+    for j in range(nb):
+        sd[p0 + "v_proj.weight"][h_e * hd + j, s_ch[j]] = 1.0
+        sd[p0 + "v_proj.weight"][h_e * hd + j, s_ref[j]] = -1.0
+    # the layer-0 LayerNorm affines of s and s' equal, so LN[s] - LN[s'] is the stem difference / sigma_t alone
+    ln0w, ln0b = sd["model.encoder.layers.0.self_attn_layer_norm.weight"], sd["model.encoder.layers.0.self_attn_layer_norm.bias"]
+    ln0w[torch.as_tensor(s_ref)] = ln0w[torch.as_tensor(s_ch)]
+    ln0b[torch.as_tensor(s_ref)] = ln0b[torch.as_tensor(s_ch)]
+    prot = torch.as_tensor(np.concatenate([m_ch, m_ref, c_ch, c_ref]))
+    for i in range(dims.n_enc_layer):
+        p = f"model.encoder.layers.{i}."
+        for w in ("self_attn.out_proj", "fc2"):
+            sd[p + w + ".weight"][prot] = 0.0
+            sd[p + w + ".bias"][prot] = 0.0
+    for j in range(nb):
+        # window-mean of (LN[s] - LN[s']) has spread ~ spread_j / 0.72 (layer-0 LN std: the sinusoid table)
+        sd[p0 + "out_proj.weight"][m_ch[j], h_e * hd + j] = float(s_enc * 0.72 / spread[j])
+
+    def same_affine(ln: str, a, b):
+        w_, b_ = sd[ln + ".weight"], sd[ln + ".bias"]
+        w_[torch.as_tensor(b)] = w_[torch.as_tensor(a)]
+        b_[torch.as_tensor(b)] = b_[torch.as_tensor(a)]
+
+    # layer-0 MLP: a saturating clip of each window bit into channel c (two GELU units per bit:
+    # o/2s * (GELU(s(Ky + 1)) - GELU(s(Ky - 1))) - o/2 = clip(Ky, -1, 1) * o/2 with the zero exactly at y = 0,
+    # since GELU(x) - GELU(-x) = x), so all but a sliver of windows carry a full-size bit
+    same_affine("model.encoder.layers.0.final_layer_norm", m_ch, m_ref)
+    pf = "model.encoder.layers.0."
+    f1w, f1b, f2w, f2b = (sd[pf + n] for n in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
+    s_g, K, o_half = 8.0, 50.0, s_enc
+    for j in range(nb):
+        for u, sgn in ((2 * j, 1.0), (2 * j + 1, -1.0)):
+            f1w[u] = 0.0
+            f1w[u, m_ch[j]] = s_g * K
+            f1w[u, m_ref[j]] = -s_g * K
+            f1b[u] = sgn * s_g
+            f2w[:, u] = 0.0
+        f2w[c_ch[j], 2 * j] = o_half / s_g
+        f2w[c_ch[j], 2 * j + 1] = -o_half / s_g
+        f2b[c_ch[j]] = -o_half
+    same_affine("model.encoder.layer_norm", c_ch, c_ref)
+
+    # ---- decoder: orthonormal directions
+    slot_dirs = len(plan.slots)
+    n_dirs = slot_dirs + nb + 4
+    q, _ = torch.linalg.qr(torch.randn(d, n_dirs, generator=g, dtype=torch.float64))
+    V = q.T.float()                                      # rows: unit, mutually orthogonal
+    v_slot = V[:slot_dirs]
+    v_bit = V[slot_dirs: slot_dirs + nb]
+    v_sot, v_en, v_eot, v_task = V[slot_dirs + nb: slot_dirs + nb + 4]
+    N = _resid_std(dims.n_dec_layer) * math.sqrt(d)     # norm of the random residual at the final LayerNorm
+    R = 6.0 * N                                         # planted token embedding norm
+    Bn = 5.0 * R                                        # successor write (> alpha * the largest bit term)
+    alpha = 0.5
+    E = sd["model.decoder.embed_tokens.weight"]
+    for k, toks in enumerate(plan.slots):
+        if len(toks) == 1:
+            E[toks[0]] = R * v_slot[k]
+        else:
+            b = v_bit[plan.bits[k]]
+            E[toks[0]] = R * (v_slot[k] + alpha * b) / math.sqrt(1 + alpha ** 2)
+            E[toks[1]] = R * (v_slot[k] - alpha * b) / math.sqrt(1 + alpha ** 2)
+    E[st.eot] = R * v_eot
+    E[st.sot] = R * v_sot
+    if dims.multilingual:
+        E[st.lang_token("en")] = R * v_en
+        E[st.transcribe] = R * v_task
+    # cross-attention head h_d of layer 1 (after the successor table, so the table's keys never see the bit
+    # terms): uniform attention reading E[m] - E[m'] into the bit directions
+    h_d = 0
+    pc = f"model.decoder.layers.{min(1, dims.n_dec_layer - 1)}.encoder_attn."
+    sl = slice(h_d * hd, (h_d + 1) * hd)
+    sd[pc + "q_proj.weight"][sl] = 0.0
+    sd[pc + "q_proj.bias"][sl] = 0.0
+    sd[pc + "v_proj.weight"][sl] = 0.0
+    sd[pc + "v_proj.bias"][sl] = 0.0
+    sd[pc + "out_proj.weight"][:, sl] = 0.0
+    S_d = 2.0 * R            # saturated window bits E[c] - E[c'] ~ +-1 -> +-2R along the bit direction
+    for j in range(nb):
+        sd[pc + "v_proj.weight"][h_d * hd + j, c_ch[j]] = 1.0
+        sd[pc + "v_proj.weight"][h_d * hd + j, c_ref[j]] = -1.0
+        sd[pc + "out_proj.weight"][:, h_d * hd + j] = S_d * v_bit[j]
+    # layer-0 MLP successor table
+    pm = "model.decoder.layers.0."
+    fc1w, fc1b = sd[pm + "fc1.weight"], sd[pm + "fc1.bias"]
+    fc2w = sd[pm + "fc2.weight"]
+    sq = math.sqrt(d)
+    gam, theta = 1.0, 0.3 * math.sqrt(d)
+    a_ref = gam * sq * 0.85 - theta                     # activation at a typical match (cos ~ 0.85)
+    units = []                                          # (key direction, write direction)
+    for k in range(len(plan.slots) - 1):
+        nxt = v_slot[k + 1]
+        if plan.kinds[k] == "ts":
+            units.append((v_slot[k], v_slot[k] + nxt))  # repeat (pair) + next text slot
+        else:
+            units.append((v_slot[k], nxt))
+    units.append((v_slot[-1], v_eot))                   # the last timestamp -> <|endoftext|>
+    if dims.multilingual:
+        units.append((v_task, v_slot[0]))
+        units.append((v_sot, v_en))                     # language detection / no-speech position
+    else:
+        units.append((v_sot, v_slot[0]))
+    for u, (key, write) in enumerate(units):
+        fc1w[u] = gam * key
+        fc1b[u] = -theta
+        fc2w[:, u] = Bn * write / a_ref
+    return plan
 
 
 def stored_as_bf16(name: str, t: torch.Tensor) -> bool:
@@ -189,12 +437,17 @@ def resolve_model(model_size_or_path: str, seed: int = 0, eot_after: Optional[in
     """-> (dims, float32 CPU state dict, model directory or None)."""
     spec = model_size_or_path
     if spec.startswith("synthetic:"):
+        # synthetic:<name>[:<seed>][:margin]  ("margin": the decisive planted program, plant_margin)
         parts = spec.split(":")
         name = parts[1]
+        plant = None
+        if parts[-1] == "margin":
+            plant = "margin"
+            parts = parts[:-1]
         if len(parts) > 2:
             seed = int(parts[2])
         dims = model_dims(name)
-        return dims, synthetic_state_dict(dims, seed, eot_after), None
+        return dims, synthetic_state_dict(dims, seed, eot_after, plant=plant), None
     if os.path.isdir(spec):
         dims, sd = load_model_dir(spec)
         return dims, sd, spec
