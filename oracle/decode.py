@@ -151,61 +151,87 @@ def generate_one(model, cross, prompt: Sequence[int], st, opt: GenerateOptions) 
 
 
 def _beam(model, cross, prompt, st, opt: GenerateOptions) -> GenerateResult:
+    return beam_many(model, cross, prompt, st, opt)[0]
+
+
+def beam_many(model, cross, prompt, st, opt: GenerateOptions) -> List[GenerateResult]:
+    """Beam search over several windows in lockstep (`cross` = model.cross_kv(enc[W])): each window's beam
+    bookkeeping is exactly the one-window search below; the decoder runs all W x K hypothesis rows at once
+    (window-major, sharing their window's cross-attention K/V).  A finished window's rows keep decoding a dummy
+    token that nothing reads."""
     K = opt.beam_size
+    W = cross[0][0].shape[0]
     max_cand = int(round(K * opt.patience))
-    last_logits, cache, no_speech = _prefill(model, cross, prompt, st)
-    # replicate the prefill state for K beams
+    toks = np.asarray([list(prompt)] * W, dtype=np.int64)
+    logits, cache = model.decode(toks, cross)
+    no_speech = [0.0] * W
+    if st.sot in prompt:
+        i = list(prompt).index(st.sot)
+        no_speech = [float(np.exp(log_softmax(logits[w, i]))[st.no_speech]) for w in range(W)]
+    # replicate each window's prefill state for its K beams (window-major rows)
     cache = [(np.repeat(k, K, 0), np.repeat(v, K, 0)) for k, v in cache]
-    logits_rows = np.repeat(last_logits[None], K, 0)
-    seqs: List[List[int]] = [[] for _ in range(K)]
-    sums = np.array([0.0] + [NEG_INF] * (K - 1))      # only beam 0 is live at the first step
-    finished: dict = {}
+    logits_rows = np.repeat(logits[:, -1], K, 0)
+    seqs = [[[] for _ in range(K)] for _ in range(W)]
+    sums = [np.array([0.0] + [NEG_INF] * (K - 1)) for _ in range(W)]   # only beam 0 is live at the first step
+    finished = [dict() for _ in range(W)]
+    done = [False] * W
     pos = len(prompt)
-    while True:
-        cands = []
-        for j in range(K):
-            if not np.isfinite(sums[j]):
-                continue
-            x = apply_rules(logits_rows[j], seqs[j], st, opt.suppress_tokens, opt.suppress_blank,
-                            opt.max_initial_timestamp_index, opt.with_timestamps)
-            lp = log_softmax(x)
-            top = np.argsort(-lp, kind="stable")[: K + 1]
-            for t in top:
-                cands.append((sums[j] + lp[t], j, int(t)))
-        cands.sort(key=lambda c: -c[0])
-        new_seqs, new_src, new_sums, new_fin = [], [], [], []
-        for score, j, t in cands:
-            if t == st.eot:
-                new_fin.append((score, tuple(seqs[j])))
-            else:
-                new_seqs.append(seqs[j] + [t]); new_src.append(j); new_sums.append(score)
-                if len(new_seqs) == K:
-                    break
-        for score, s in new_fin:
-            if len(finished) >= max_cand:
-                break
-            finished.setdefault(s, score)
+    while not all(done):
+        src_all = np.arange(W * K)
+        last = np.full(W * K, st.eot, dtype=np.int64)
         pos += 1
-        if len(finished) >= max_cand or pos >= opt.max_length or not new_seqs:
-            if len(finished) < K:
-                for score, s in sorted(zip(new_sums, new_seqs), key=lambda z: -z[0]):
-                    if len(finished) >= K:
+        for w in range(W):
+            if done[w]:
+                continue
+            cands = []
+            for j in range(K):
+                if not np.isfinite(sums[w][j]):
+                    continue
+                x = apply_rules(logits_rows[w * K + j], seqs[w][j], st, opt.suppress_tokens, opt.suppress_blank,
+                                opt.max_initial_timestamp_index, opt.with_timestamps)
+                lp = log_softmax(x)
+                top = np.argsort(-lp, kind="stable")[: K + 1]
+                for t in top:
+                    cands.append((sums[w][j] + lp[t], j, int(t)))
+            cands.sort(key=lambda c: -c[0])
+            new_seqs, new_src, new_sums, new_fin = [], [], [], []
+            for score, j, t in cands:
+                if t == st.eot:
+                    new_fin.append((score, tuple(seqs[w][j])))
+                else:
+                    new_seqs.append(seqs[w][j] + [t]); new_src.append(j); new_sums.append(score)
+                    if len(new_seqs) == K:
                         break
-                    finished.setdefault(tuple(s), score)
+            for score, sq in new_fin:
+                if len(finished[w]) >= max_cand:
+                    break
+                finished[w].setdefault(sq, score)
+            if len(finished[w]) >= max_cand or pos >= opt.max_length or not new_seqs:
+                if len(finished[w]) < K:
+                    for score, sq in sorted(zip(new_sums, new_seqs), key=lambda z: -z[0]):
+                        if len(finished[w]) >= K:
+                            break
+                        finished[w].setdefault(tuple(sq), score)
+                done[w] = True
+                continue
+            while len(new_seqs) < K:
+                new_seqs.append(list(new_seqs[0])); new_src.append(new_src[0]); new_sums.append(NEG_INF)
+            src_all[w * K:(w + 1) * K] = w * K + np.asarray(new_src)
+            last[w * K:(w + 1) * K] = [sq[-1] for sq in new_seqs]
+            seqs[w] = new_seqs
+            sums[w] = np.asarray(new_sums)
+        if all(done):
             break
-        while len(new_seqs) < K:
-            new_seqs.append(list(new_seqs[0])); new_src.append(new_src[0]); new_sums.append(NEG_INF)
-        src = np.asarray(new_src)
-        cache = [(k[src], v[src]) for k, v in cache]
-        seqs = new_seqs
-        sums = np.asarray(new_sums)
-        toks = np.asarray([[s[-1]] for s in seqs])
-        logits, cache = model.decode(toks, cross, cache, offset=pos - 1)
+        cache = [(k[src_all], v[src_all]) for k, v in cache]
+        logits, cache = model.decode(last[:, None], cross, cache, offset=pos - 1)
         logits_rows = logits[:, -1]
-    ranked = sorted(finished.items(), key=lambda kv: -_norm(kv[1], len(kv[0]), opt.length_penalty))
-    best, cum = ranked[0]
-    return GenerateResult(list(best), _norm(cum, len(best), opt.length_penalty), no_speech, cum,
-                          [list(s) for s, _ in ranked])
+    out = []
+    for w in range(W):
+        ranked = sorted(finished[w].items(), key=lambda kv: -_norm(kv[1], len(kv[0]), opt.length_penalty))
+        best, cum = ranked[0]
+        out.append(GenerateResult(list(best), _norm(cum, len(best), opt.length_penalty), no_speech[w], cum,
+                                  [list(sq) for sq, _ in ranked]))
+    return out
 
 
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)

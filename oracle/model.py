@@ -101,7 +101,7 @@ class OracleWhisper:
         return x.transpose(0, 2, 1, 3).reshape(B, T, H * hd)
 
     def _attn(self, q, k, v, mask=None, return_weights=False):
-        s = (q @ k.transpose(0, 1, 3, 2)) / np.sqrt(self.hd).astype(self.dtype)
+        s = (q @ np.swapaxes(k, -1, -2)) / np.sqrt(self.hd).astype(self.dtype)
         if mask is not None:
             s = s + mask
         p = softmax(s, -1)
@@ -199,11 +199,16 @@ class OracleWhisper:
             h = self._q(layer_norm(x, w[p + "encoder_attn_layer_norm.weight"], w[p + "encoder_attn_layer_norm.bias"]))
             q = self._split(self._q(self._lin(h, p + "encoder_attn.q_proj")))
             ck, cv = cross[i]
-            if ck.shape[0] not in (1, B):   # hypotheses sharing one window's cross-KV (beam search);
-                # a single window broadcasts through the batched matmuls without a copy
-                rep = B // ck.shape[0]
-                ck, cv = np.repeat(ck, rep, axis=0), np.repeat(cv, rep, axis=0)
-            o, pw = self._attn(q, ck, cv, return_weights=return_cross_attn)
+            if ck.shape[0] not in (1, B):   # hypotheses sharing their window's cross-KV (beam search): rows are
+                # window-major groups of `rep`; broadcast each window's K/V over its group without a copy
+                nw = ck.shape[0]
+                rep = B // nw
+                qg = q.reshape(nw, rep, *q.shape[1:])
+                o, pw = self._attn(qg, ck[:, None], cv[:, None], return_weights=return_cross_attn)
+                o = o.reshape(B, *o.shape[2:])
+                pw = pw.reshape(B, *pw.shape[2:]) if pw is not None else None
+            else:
+                o, pw = self._attn(q, ck, cv, return_weights=return_cross_attn)
             if return_cross_attn:
                 cross_w.append(pw)
             x = x + self._lin(self._q(self._merge(o)), p + "encoder_attn.out_proj")

@@ -150,6 +150,14 @@ GATE_WER = 0.003           # WER delta <= 0.3 % absolute
 GATE_DT = 0.02             # segment start / end within one timestamp token (20 ms)
 
 
+def progress(msg: str) -> None:
+    """One line to $VLOG_AMD_PROGRESS (long oracle checks on the GPU box keep a file under gpurun_out/ moving)."""
+    path = os.environ.get("VLOG_AMD_PROGRESS")
+    if path:
+        with open(path, "a") as f:
+            f.write(msg + "\n")
+
+
 def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists: Sequence[Sequence[int]],
                         ended: Sequence[bool], st, opt: GenerateOptions):
     """Several windows in ONE oracle decoder pass (sequences padded with <|endoftext|>: the mask is causal, so
@@ -168,11 +176,12 @@ def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists
         seq = list(t) + ([st.eot] if ended[i] else [])
         ms = np.empty(len(seq))
         for k, tok in enumerate(seq):
-            lp = log_softmax(apply_rules(logits[i, P - 1 + k], list(t[:k]), st, opt.suppress_tokens, opt.suppress_blank,
-                                         opt.max_initial_timestamp_index, opt.with_timestamps))
-            chosen = lp[tok]
-            lp[tok] = -np.inf
-            ms[k] = chosen - np.max(lp)
+            # the margin of the rule-masked logits equals that of their log-softmax (same shift)
+            x = apply_rules(logits[i, P - 1 + k], list(t[:k]), st, opt.suppress_tokens, opt.suppress_blank,
+                            opt.max_initial_timestamp_index, opt.with_timestamps)
+            chosen = x[tok]
+            x[tok] = -np.inf
+            ms[k] = chosen - np.max(x) if np.isfinite(chosen) else -np.inf
         assert not np.isnan(ms).any()
         ns = 0.0
         if st.sot in prompt:
@@ -193,10 +202,13 @@ def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateO
     from vlog_amd.segments import split_segments_by_timestamps
     from oracle.decode import generate_one
 
+    import time
     ws = list(range(len(results))) if windows is None else list(windows)
     ident, margins, ns_diff, non_ident = [], [], 0.0, []
     oracle_tokens = {}
+    t0 = time.time()
     for c0 in range(0, len(ws), chunk):
+        progress(f"gate_windows: {c0}/{len(ws)} windows checked, {time.time() - t0:.1f} s")
         cw = ws[c0:c0 + chunk]
         enc = enc_of(cw)
         toks = [list(results[w].tokens) for w in cw]
@@ -210,6 +222,7 @@ def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateO
                 margins.append(float(np.min(ms)) if ms.size else 0.0)
             else:
                 non_ident.append(w)
+                progress(f"gate_windows: window {w} not identical: oracle greedy re-decode")
                 r = generate_one(orc, orc.cross_kv(enc[j:j + 1]), prompt, st, opt)
                 oracle_tokens[w] = list(r.tokens)
     errs, n_ref, dt, seg_mismatch = 0, 0, 0.0, 0

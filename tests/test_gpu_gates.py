@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle.decode import GenerateOptions, generate_one
+from oracle.decode import GenerateOptions, beam_many
 from oracle.model import OracleWhisper
 from tests.parity_util import GATE_IDENTICAL, assert_gates, gate_windows, sample_indices
 from vlog_amd.audio import speech_like
@@ -133,11 +133,10 @@ def test_config5_beam5_identical_to_oracle_beam(lv3):
     finally:
         lv3.eng.set_option("cross_mode", 1)
     ws = sample_indices(W, 8)
-    same = []
-    for w in ws:
-        enc = lv3.enc_of([w])
-        r = generate_one(lv3.orc, lv3.orc.cross_kv(enc), lv3.prompt, lv3.st, lv3.opt(beam=5))
-        same.append(r.tokens == list(res[w].tokens))
+    from tests.parity_util import progress
+    progress("beam5: oracle beam search over 8 windows")
+    refs = beam_many(lv3.orc, lv3.orc.cross_kv(lv3.enc_of(ws)), lv3.prompt, lv3.st, lv3.opt(beam=5))
+    same = [r.tokens == list(res[w].tokens) for w, r in zip(ws, refs)]
     g = gate_windows(lv3.orc, lv3.enc_of, lv3.prompt, res, lv3.st, lv3.opt(beam=5), lv3.tok, windows=ws)
     _record("gates large-v3 beam5 128 windows (8 sampled vs oracle beam)", dict(g, identical_to_oracle_beam=sum(same)))
     assert all(same), (ws, same)

@@ -5,7 +5,7 @@ R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
 TAG=${TAG:-step}
 TESTS=${TESTS:-tests/test_gpu_gates.py}
-export VLOG_AMD_PARITY_OUT=$R/gpurun_out/parity_$TAG.jsonl
+export VLOG_AMD_PARITY_OUT=$R/gpurun_out/parity_$TAG.jsonl VLOG_AMD_PROGRESS=$R/gpurun_out/progress_$TAG.log
 if [ "$TESTS" != "none" ]; then
   timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest $TESTS -x -v --timeout 600 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
   rc=$?; tail -3 gpurun_out/tests_$TAG.log

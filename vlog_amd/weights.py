@@ -146,25 +146,19 @@ def plant_eot(sd: Dict[str, torch.Tensor], dims: ModelDims, eot_after: int, seed
 
 
 # ----------------------------------------------------------------------------- margin-planted synthetic model
-# Per-window statistics of the seeded speech-like corpus (vlog_amd.audio.speech_like, 64 clips, normalised log-mel
-# as the encoder sees it): for each bit feature, the median over windows of the window-mean projection.  Feature 0
-# is the mean over all mel bins; features 1.. are zero-sum random projections (seed 1234, normalised to unit L1).
-# Recomputed by tools/calibrate_margin.py; only the centring of the bits depends on them.
-_BIT_MEDIANS = {80: (-0.2237, 0.0275, 0.0225, 0.0088, 0.0052, -0.0086),
-                128: (-0.2134, 0.0053, -0.0107, 0.0021, 0.0039, -0.0023)}
-_BIT_SPREADS = {80: (0.0546, 0.0038, 0.0035, 0.0014, 0.0013, 0.0017),
-                128: (0.0472, 0.0013, 0.0020, 0.0014, 0.0011, 0.0013)}
+# The audio bits: window-level features of the normalised log-mel (projections of the window-mean spectrum onto
+# the corpus' leading principal components, so the bits are uncorrelated over windows), centred on the corpus
+# median.  vlog_amd/margin_calib.json, written by tools/calibrate_margin.py; only the centring and scale of the
+# bits depend on it.
 N_BITS = 6
 
 
-def bit_projections(n_mels: int) -> np.ndarray:
-    """[n_mels, N_BITS] mel-bin weights of the bit features (see _BIT_MEDIANS)."""
-    rng = np.random.default_rng(1234)
-    p = rng.standard_normal((n_mels, N_BITS))
-    p -= p.mean(0)
-    p /= np.abs(p).sum(0)
-    p[:, 0] = 1.0 / n_mels
-    return p
+def _margin_calib(n_mels: int) -> dict:
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "margin_calib.json")) as f:
+        t = json.load(f)["tables"]
+    if str(n_mels) not in t:
+        raise ValueError(f"no margin-model calibration for n_mels={n_mels}")
+    return t[str(n_mels)]
 
 
 @dataclass
@@ -248,9 +242,11 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
     nb = N_BITS
     ch = rng.choice(d, size=6 * nb, replace=False)
     s_ch, s_ref, m_ch, m_ref, c_ch, c_ref = (ch[i * nb:(i + 1) * nb] for i in range(6))
-    P = torch.from_numpy(bit_projections(dims.n_mels)).float()          # [n_mels, nb]
-    med = _BIT_MEDIANS.get(dims.n_mels, (0.0,) * nb)
-    spread = _BIT_SPREADS.get(dims.n_mels, (0.01,) * nb)
+    cal = _margin_calib(dims.n_mels)
+    P = torch.tensor(cal["proj"], dtype=torch.float32)               # [n_mels, nb]
+    med, fstd = cal["median"], cal["frame_std"]
+    g1 = [0.25 / f for f in fstd]                                    # 4 frame-sigma -> GELU argument +-1 around b1
+    spread = [g * sp for g, sp in zip(g1, cal["spread"])]
     b1 = 3.0
     c1w, c1b = sd["model.encoder.conv1.weight"], sd["model.encoder.conv1.bias"]       # [d, n_mels, 3]
     c2w, c2b = sd["model.encoder.conv2.weight"], sd["model.encoder.conv2.bias"]       # [d, d, 3]
@@ -258,8 +254,8 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
     for j in range(nb):
         for c in (s_ch[j], s_ref[j], m_ch[j], m_ref[j], c_ch[j], c_ref[j]):
             c1w[c] = 0.0; c1b[c] = 0.0; c2w[c] = 0.0; c2b[c] = 0.0
-        c1w[s_ch[j], :, 1] = P[:, j]
-        c1b[s_ch[j]] = b1 - float(med[j])
+        c1w[s_ch[j], :, 1] = g1[j] * P[:, j]
+        c1b[s_ch[j]] = b1 - g1[j] * float(med[j])
         c1b[s_ref[j]] = b1
         c2w[s_ch[j], s_ch[j], 1] = 1.0                   # GELU(y + b1) - GELU(b1) + b1 through the second GELU
         c2w[s_ref[j], s_ref[j], 1] = 1.0
