@@ -214,6 +214,7 @@ def parity_sample(dims, sd, pipe, fp8_cross: bool = False) -> dict:
     ws = sorted(enc)
     g = gate_windows(orc, lambda w: np.stack([enc[i] for i in w]), pipe.prompt, res, dims.specials, opt, pipe.tok,
                      windows=ws, time_offset=lambda w: (pipe.rank * pipe.W + w) * 30.0)
+    g.pop("oracle_tokens")
     g["windows"] = ws
     g["method"] = ("every sampled window's GPU tokens teacher-forced through oracle/ (bf16-activation mode) on the "
                    "GPU's encoder output; identical = the GPU token is the oracle's argmax at every step; "

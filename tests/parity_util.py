@@ -191,13 +191,17 @@ def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists
 
 
 def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateOptions, tokenizer,
-                 windows: Optional[Sequence[int]] = None, chunk: int = 8, time_offset=lambda w: 0.0) -> dict:
+                 windows: Optional[Sequence[int]] = None, chunk: int = 8, time_offset=lambda w: 0.0,
+                 known: Optional[dict] = None) -> dict:
     """The north_star parity gates over every window (or `windows`): each GPU token sequence is teacher-forced
     through the oracle (identical = the GPU token is the oracle's argmax at every step, so the oracle's greedy
     search produces exactly that sequence); windows that are not identical are re-decoded by the oracle's own
     greedy search.  WER delta = WER of the GPU transcript against the oracle transcript (per-window edit
     distances summed); segment times compared segment by segment (start/end within 20 ms).
-    enc_of(list of window ids) -> float32 [n, 1500, d] (the GPU's encoder output: parity at the decoder)."""
+    enc_of(list of window ids) -> float32 [n, 1500, d] (the GPU's encoder output: parity at the decoder).
+    known: {window: oracle greedy tokens} already established for the SAME encoder output, weights and options
+    (a previous gate_windows call's "oracle_tokens"); a window whose GPU tokens equal them is identical without
+    another oracle pass."""
     from vlog_amd.metrics import edit_distance, normalize
     from vlog_amd.segments import split_segments_by_timestamps
     from oracle.decode import generate_one
@@ -207,9 +211,16 @@ def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateO
     ident, margins, ns_diff, non_ident = [], [], 0.0, []
     oracle_tokens = {}
     t0 = time.time()
-    for c0 in range(0, len(ws), chunk):
-        progress(f"gate_windows: {c0}/{len(ws)} windows checked, {time.time() - t0:.1f} s")
-        cw = ws[c0:c0 + chunk]
+    todo = []
+    for w in ws:
+        if known is not None and w in known and list(results[w].tokens) == list(known[w]):
+            ident.append(True)
+            oracle_tokens[w] = list(known[w])
+        else:
+            todo.append(w)
+    for c0 in range(0, len(todo), chunk):
+        progress(f"gate_windows: {c0}/{len(todo)} windows checked, {time.time() - t0:.1f} s")
+        cw = todo[c0:c0 + chunk]
         enc = enc_of(cw)
         toks = [list(results[w].tokens) for w in cw]
         ended = [len(prompt) + len(t) < opt.max_length for t in toks]
@@ -242,7 +253,8 @@ def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateO
             "wer_delta": round(errs / max(n_ref, 1), 6), "segment_max_dt_s": round(dt, 4),
             "segment_count_mismatch": seg_mismatch, "max_no_speech_diff": ns_diff,
             "min_margin_identical_nats": round(min(margins), 3) if margins else None,
-            "non_identical_windows": non_ident,
+            "non_identical_windows": non_ident, "oracle_passes": len(todo),
+            "oracle_tokens": oracle_tokens,
             "gates": {"identical_frac": GATE_IDENTICAL, "wer_delta": GATE_WER, "segment_dt_s": GATE_DT}}
 
 

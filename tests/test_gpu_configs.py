@@ -1,4 +1,6 @@
-"""Parity of the BASELINE.json configurations, at the sizes the bench runs, against the CPU oracle.
+"""Stress tests on RANDOM-init weights (near-tied logits) at the sizes the bench runs, against the CPU oracle.
+The north_star gates themselves (identity / WER / timestamps on every window) run on the margin-planted model
+in tests/test_gpu_gates.py; these keep the kernels honest where logits are NOT decisive.
 
 Each config decodes its full batch on the MI355X (so the kernel instantiations the bench uses run — for
 large-v3 greedy that is 150 decoder rows, the M <= 160 GEMM / ring / factored cross-attention paths), then
@@ -120,65 +122,8 @@ def test_large_v3_encoder_vs_bf16_oracle(lv3):
         assert mean < 0.004 * rms + 0.002, errs
 
 
-def test_large_v3_beam5_128_windows_vs_oracle(lv3):
-    """Config 5's search: beam 5 over 128 windows (640 hypothesis rows).  The GPU's chosen hypothesis must be
-    epsilon-optimal against the oracle's own beam search (openai BeamSearchDecoder semantics) and identical to
-    it on most sampled windows."""
-    W = 128
-    lv3.eng.reserve(150, W * 5)
-    lv3.eng.cross_kv(lv3.enc, 0)
-    res, steps = lv3.eng.generate(list(range(W)), [lv3.prompt] * W, beam_size=5, patience=1.0,
-                                  suppress_tokens=lv3.sup, max_length=448, check_every=8)
-    assert len(res) == W
-    eps = EPS["large-v3"]
-    rows, same = [], 0
-    for w in sample_indices(W, 3):
-        cross = lv3.orc.cross_kv(lv3.enc_window(w)[None])
-        r = generate_one(lv3.orc, cross, lv3.prompt, lv3.st, lv3.opt(beam=5))
-        g = window_parity(lv3.orc, lv3.enc_window(w), lv3.prompt, res[w], lv3.st, lv3.opt(beam=5), w, eps=eps)
-        same += r.tokens == res[w].tokens
-        rows.append(dict(window=w, identical=r.tokens == res[w].tokens, score_gpu_seq=g.score_oracle,
-                         score_oracle_beam=r.score, score_gpu=res[w].score, n_gpu=len(res[w].tokens),
-                         n_oracle=len(r.tokens), worst_tie_margin=g.min_margin_rule_tie))
-        assert np.isfinite(g.min_margin_rule_tie), rows[-1]      # every token allowed by the rules (ties aside)
-        assert g.score_oracle >= r.score - eps, rows[-1]         # the GPU's hypothesis is eps-optimal
-        assert abs(g.score_oracle - res[w].score) < 2e-2 * max(1.0, abs(g.score_oracle)), rows[-1]
-        assert abs(g.no_speech_oracle - res[w].no_speech_prob) < 1e-3
-    import os, json
-    p = os.environ.get("VLOG_AMD_PARITY_OUT")
-    if p:
-        with open(p, "a") as f:
-            f.write(json.dumps({"name": "large-v3 beam5 128 windows", "identical": same, "n": len(rows),
-                                "steps": steps, "windows": rows}) + "\n")
-
-
-def test_large_v3_fp8_cross_memory_150_windows_vs_oracle(lv3):
-    """Opt-in fp8 cross memory at the bench size: the quantiser bit-exact at n_state 1280, then 150 windows
-    greedy in fp8 mode vs the oracle on the dequantised encoder output; token agreement with the bf16 mode is
-    recorded (it measures the fp8 approximation, not kernel correctness)."""
-    from oracle import fp8
-    codes, scale = lv3.eng.cross_fp8_quantize(lv3.enc[:2])
-    rc, rs, _ = fp8.quantize_rows(lv3.enc[:2].reshape(-1, lv3.dims.n_state).float().cpu().numpy())
-    assert np.array_equal(scale.cpu().numpy(), rs) and np.array_equal(codes.cpu().numpy(), rc)
-    ref, _ = lv3.greedy()
-    lv3.eng.set_option("cross_fp8", 1)
-    try:
-        res, steps = lv3.greedy()
-    finally:
-        lv3.eng.set_option("cross_fp8", 0)
-    eps = EPS["large-v3"]
-    rows = []
-    for w in sample_indices(lv3.W, 6):
-        deq = fp8.quantize_rows(lv3.enc_window(w))[2]
-        rows.append(window_parity(lv3.orc, deq, lv3.prompt, res[w], lv3.st, lv3.opt(), w, eps=eps))
-    from vlog_amd.metrics import edit_distance
-    same = sum(a.tokens == b.tokens for a, b in zip(res, ref))
-    w_delta = sum(edit_distance(b.tokens, a.tokens) for a, b in zip(res, ref)) / max(1, sum(len(b.tokens) for b in ref))
-    record("large-v3 fp8 cross memory 150 windows", rows, steps=steps, identical_to_bf16_mode=same,
-           token_wer_vs_bf16_mode=w_delta, eps=eps)
-    for r in rows:
-        assert r.min_margin_rule_tie >= -eps, (r.window, r.min_margin_rule_tie, r.worst_step, r.worst_gap)
-        assert abs(r.no_speech_gpu - r.no_speech_oracle) < 1e-3
+# Config 5's beam search and the opt-in fp8 cross memory are gated on the margin-planted model
+# (tests/test_gpu_gates.py: identity with the oracle's own beam search; fp8 vs the full-precision oracle).
 
 
 # ------------------------------------------------------------------------------------------ configs 2 and 3

@@ -9,7 +9,7 @@ R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
 TAG=${TAG:-r03}
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --durations=20 --timeout 600 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
   rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log
   [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" gpurun_out/gpu_tests_$TAG.log | head -30; exit $rc; }
 fi

@@ -7,7 +7,7 @@ TAG=${TAG:-step}
 TESTS=${TESTS:-tests/test_gpu_gates.py}
 export VLOG_AMD_PARITY_OUT=$R/gpurun_out/parity_$TAG.jsonl VLOG_AMD_PROGRESS=$R/gpurun_out/progress_$TAG.log
 if [ "$TESTS" != "none" ]; then
-  timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest $TESTS -x -v --timeout 600 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
+  timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest $TESTS -x -v --durations=15 --timeout 600 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
   rc=$?; tail -3 gpurun_out/tests_$TAG.log
   [ $rc -ne 0 ] && { grep -E "FAILED|Error|^E " gpurun_out/tests_$TAG.log | head -30; exit $rc; }
 fi
