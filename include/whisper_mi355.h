@@ -198,6 +198,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   slice's weight GEMMs overlapping the other's cross-attention.  Results are bit-identical
  *   either way; off by default because the overlap measured slower on MI355X (the GEMM blocks queue behind
  *   the cross-attention blocks).
+ *   "decode_graph" (default 1): after one eager decode step, wm_generate captures a step (decoder pass +
+ *   token selection) as a HIP graph and replays it for the remaining steps (every per-step quantity lives in
+ *   device memory).  Bit-identical either way; off while the event profiler is on or with "decode_split".
  *   "decode_ring_gemm" (default 1): 0 disables the all-rows ring GEMM (plan value 0 below falls back to the
  *   split-K skinny GEMM).
  *   "decode_gemm_plan" (default 1): preset routing of the six decoder projections (qkv, out, cq, cout, fc1, fc2)

@@ -94,6 +94,19 @@ def test_split_decode_bit_identical(batch, kw):
     assert sum(len(r.tokens) for r in a) > W * 5
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0),
+                                dict(temperature=0.6, num_hypotheses=5, seed=7)], ids=["greedy", "beam5", "sampling"])
+def test_step_graph_replay_bit_identical(batch, kw):
+    """Decode steps replayed from one captured HIP graph (decode_graph=1, the default) vs launched eagerly: the
+    same tokens, scores and no-speech probabilities (sampling keys its Gumbel noise on the device-side step)."""
+    dims, eng = batch
+    a, sa = _run(eng, dims, 0, opts=(("decode_graph", 0),), **kw)
+    eng.set_option("decode_graph", 1)
+    b, sb = _run(eng, dims, 0, **kw)
+    _same(a, sa, b, sb)
+    assert sum(len(r.tokens) for r in a) > W * 5
+
+
 def test_unknown_option_raises(batch):
     _, eng = batch
     with pytest.raises(RuntimeError, match="unknown option"):

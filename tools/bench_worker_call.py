@@ -7,10 +7,11 @@
 
 timed from the call to the VTT string, in the default sequential mode (faster-whisper seek loop) and in the
 opt-in throughput mode (VLOG_AMD_THROUGHPUT=1 -> BatchedInferencePipeline).  Reports RTFx of each and the WER
-of the throughput transcript against the sequential one on the same clip.  Synthetic large-v3 weights: the
-random model's average log-probability (about -7) is below faster-whisper's -1.0 threshold on every window, so
-the default temperature fallback re-decodes every window at five temperatures (best_of 5) in both modes —
-the worker's call as written, on this model.  Prints one JSON line.
+of the throughput transcript against the sequential one on the same clip.  Synthetic large-v3 weights with the
+margin-planted decoder program (decisive like a trained model: windows pass faster-whisper's thresholds at
+temperature 0, so the default fallback ladder costs nothing extra); --random-weights: plain random init, whose
+average log-probability (about -7) fails the -1.0 threshold on every window, so the fallback re-decodes every
+window at five temperatures (best_of 5).  Prints one JSON line.
 usage: python tools/bench_worker_call.py [--minutes-seq 5] [--minutes-tp 60] [--model large-v3]
 """
 import argparse
@@ -53,8 +54,15 @@ def main():
     ap.add_argument("--temperature", type=float, default=None,
                     help="fixed temperature (e.g. 0: no fallback ladder, the cost of the call on a model whose windows "
                          "pass faster-whisper's thresholds); default: the worker's call as written")
+    ap.add_argument("--random-weights", action="store_true",
+                    help="plain random-init weights (every window fails the log-prob threshold and is re-decoded at "
+                         "five temperatures); default: the margin-planted model, whose windows pass like a trained one")
+    ap.add_argument("--no-graph", action="store_true", help="decode steps launched eagerly (decode_graph=0)")
     args = ap.parse_args()
-    model = WhisperModel(f"synthetic:{args.model}:0", device="cpu", compute_type="int8", eot_after=110)
+    spec = f"synthetic:{args.model}:0" + ("" if args.random_weights else ":margin")
+    model = WhisperModel(spec, device="cpu", compute_type="int8", eot_after=110)
+    if args.no_graph:
+        model.engine.set_option("decode_graph", 0)
     tmp = tempfile.mkdtemp()
 
     def clip(minutes, name):
@@ -65,7 +73,7 @@ def main():
 
     short, short_s = clip(args.minutes_seq, "short.wav")
     long_, long_s = clip(args.minutes_tp, "long.wav")
-    out = {"model": args.model, "call": "transcribe(str(wav), language=None, task='transcribe', beam_size=5, "
+    out = {"model": args.model, "weights": spec, "decode_graph": not args.no_graph, "call": "transcribe(str(wav), language=None, task='transcribe', beam_size=5, "
                                         "vad_filter=True) + generate_webvtt"}
     T = args.temperature
     if T is not None:

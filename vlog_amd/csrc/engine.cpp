@@ -165,6 +165,9 @@ struct wm_engine {
   int dec_cols[6] = {32, 32, 32, 32, 64, 64};   // ring GEMM output columns per block (32 or 64)
   int dec_kr[6] = {0, 0, 0, 0, 0, 0};           // ring GEMM K range per block (0: the whole K up to 1280)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
+  int dec_graph = 1;         // decode steps replayed from one captured HIP graph (see generate)
+  hipStream_t gst = nullptr; // the capture / replay stream (a graph cannot be captured on the legacy null stream)
+  hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr;
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
                              // the cross-attention kernel; bit 1 measured slower (per-item hand-off latency)
   DevBuf d_cross_cnt;        // its per-(row, head) arrival counters (zeroed at allocation, reset in-kernel)
@@ -849,20 +852,82 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   int steps = 1;
   const int max_steps = a->max_length - P;      // generated tokens (incl. the final one) <= max_length - P
   const int check = std::max(1, a->check_every);
-  for (int step = 1; step < max_steps; ++step) {
-    if ((step - 1) % check == 0) {
-      int act = 0;
-      HIP_OK(hipMemcpyAsync(&act, e->d_n_active.p, 4, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      if (act <= 0) break;
+  // A decode step's launches are identical from step to step: every per-step quantity (tokens, positions,
+  // lineage, done flags, sequence lengths) lives in device memory and is advanced by the select kernels, so
+  // after one eager step (which sizes every scratch buffer) the step is captured once as a HIP graph and
+  // replayed: one graph launch per step instead of ~11 kernel launches per layer.  Not with the event profiler
+  // (its events are per launch) or the two-stream split.  The replay stream is joined to `st` before every
+  // host poll and at the end.
+  const bool use_graph = e->dec_graph && !e->prof_on && !e->dec_split;
+  hipGraphExec_t gexec = nullptr;
+  bool capturing = false;
+  hipStream_t ds = st;
+  if (use_graph) {
+    if (!e->gst) {
+      HIP_OK(hipStreamCreateWithFlags(&e->gst, hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_g0, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_g1, hipEventDisableTiming));
     }
+    HIP_OK(hipEventRecord(e->ev_g0, st));
+    HIP_OK(hipStreamWaitEvent(e->gst, e->ev_g0, 0));
+    ds = e->gst;
+  }
+  auto step_eager = [&](int step, hipStream_t s) {
     // logits rows of a decode step are the hypotheses themselves
     // greedy / sampling never reorder hypotheses: the lineage table is the identity and self-attention
     // reads each row's own cache directly (no dependent lineage load per key block)
     decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                 beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, st);
-    select(step);
-    ++steps;
+                 beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, s);
+    sp.step = step;
+    launch_logits_select(sp, NH, s);
+    if (beam) launch_beam_select(bp, W, s);
+  };
+  try {
+    for (int step = 1; step < max_steps; ++step) {
+      if ((step - 1) % check == 0) {
+        int act = 0;
+        HIP_OK(hipMemcpyAsync(&act, e->d_n_active.p, 4, hipMemcpyDeviceToHost, ds));
+        HIP_OK(hipStreamSynchronize(ds));
+        if (act <= 0) break;
+      }
+      if (!use_graph || step == 1) {
+        if (use_graph) step_eager(step, ds);
+        else {
+          decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
+                       beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, st);
+          select(step);
+        }
+      } else {
+        if (!gexec) {
+          hipGraph_t g = nullptr;
+          HIP_OK(hipStreamBeginCapture(ds, hipStreamCaptureModeThreadLocal));
+          capturing = true;
+          step_eager(step, ds);
+          capturing = false;
+          HIP_OK(hipStreamEndCapture(ds, &g));
+          const hipError_t ie = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+          (void)hipGraphDestroy(g);
+          HIP_OK(ie);
+        }
+        HIP_OK(hipGraphLaunch(gexec, ds));
+      }
+      ++steps;
+    }
+  } catch (...) {
+    if (capturing) {                           // leave the stream out of capture mode before reporting
+      hipGraph_t g = nullptr;
+      if (hipStreamEndCapture(ds, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+    }
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    throw;
+  }
+  if (use_graph) {
+    HIP_OK(hipEventRecord(e->ev_g1, ds));
+    HIP_OK(hipStreamWaitEvent(st, e->ev_g1, 0));
+  }
+  if (gexec) {
+    HIP_OK(hipStreamSynchronize(ds));          // the graph's last replay has completed before it is destroyed
+    HIP_OK(hipGraphExecDestroy(gexec));
   }
 
   // ---- results
@@ -1168,6 +1233,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     e->dm = *dims;
     e->device = device;
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_GRAPH")) e->dec_graph = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_PLAN")) {
       const int p = std::atoi(v) != 0;
@@ -1228,6 +1294,9 @@ void wm_destroy(wm_engine* e) {
                     &e->a_pj, &e->a_plen, &e->a_meta})
     b->release();
   if (e->st2) (void)hipStreamDestroy(e->st2);
+  if (e->gst) (void)hipStreamDestroy(e->gst);
+  if (e->ev_g0) (void)hipEventDestroy(e->ev_g0);
+  if (e->ev_g1) (void)hipEventDestroy(e->ev_g1);
   for (hipEvent_t ev : {e->ev_fork, e->ev_mid, e->ev_join})
     if (ev) (void)hipEventDestroy(ev);
   delete e;
@@ -1440,6 +1509,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     if (!key) throw std::runtime_error("wm_set_option: null key");
     const std::string k(key);
     if (k == "decode_split") e->dec_split = value != 0;
+    else if (k == "decode_graph") e->dec_graph = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
     else if (k == "decode_gemm_plan") {
       if (value != 0 && value != 1) throw std::runtime_error("wm_set_option: decode_gemm_plan is 0 or 1");

@@ -186,7 +186,9 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
     Cand& m = is_ts ? ms : mt;
     if (better(x, i, m.v, m.i)) { m.v = x; m.i = i; }
     if (MODE == 2) {
-      const float key = x * p.inv_temperature + gumbel(p.seed, h, p.step, i);
+      // the decode step of this hypothesis = tokens it has sampled so far (equal to the host's step counter
+      // for every live hypothesis; read from the device so a captured step graph replays unchanged)
+      const float key = x * p.inv_temperature + gumbel(p.seed, h, len - p.sample_begin, i);
       Cand& gg = is_ts ? gs : gt;
       if (better(key, i, gg.v, gg.i)) { gg.v = key; gg.i = i; }
     } else if (MODE == 1) {
