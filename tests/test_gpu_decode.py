@@ -348,15 +348,13 @@ def test_batched_pipeline_matches_single_window_decode():
     wins = pipe.fixed_windows(feats.shape[1] - 1)
     results = pipe.decode_windows(feats, wins, [s * 0.01 for s, _ in wins], tok, opts)
     assert len(results) == 6 and wins[-1][1] == 700
-    # the batched call decoded in the projected cross-attention form (best_of 5 groups, transcribe.py auto form)
-    # and restored the engine's form afterwards; compare in the same form
-    model.engine.set_option("cross_mode", 0)
+    # greedy: the batched call chose the factored cross-attention form (transcribe.py _use_cross_form), the
+    # engine's default, which the single-window calls below use too
     for (seek, size), wr in zip(wins, results):
         enc = model.engine.encode(feats, [seek], [size])
         model.engine.cross_kv(enc, 0)
         res, _ = model.engine.generate([0], [tok.sot_sequence], suppress_tokens=opts.suppress_tokens, max_length=448)
         assert wr.tokens == res[0].tokens
-    model.engine.set_option("cross_mode", 1)
     segs, info = pipe.transcribe(x, language="en", beam_size=1, temperature=0.0, vad_filter=False,
                                  without_timestamps=False)
     segs = list(segs)

@@ -225,6 +225,16 @@ class WhisperModel:
     def _features(self, audio: np.ndarray) -> torch.Tensor:
         return self.engine.features(torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)))
 
+    def _use_cross_form(self, rows_per_window: int) -> None:
+        """Cross-attention form for decodes with `rows_per_window` rows per window: the factored form (attention
+        over the encoder output; half the bytes of K and V) for one row, the projected K/V form when several
+        rows share a window (beam search: every row of the group reads the window's K/V panels once, while the
+        factored kernel re-reads the encoder output per 32 (row, head) pairs).  The opt-in fp8
+        cross memory is a factored-form mode and is never overridden; VLOG_AMD_CROSS_AUTO=0 disables the choice."""
+        if os.environ.get("VLOG_AMD_CROSS_AUTO", "1") == "0" or self.engine.option("cross_fp8", 0):
+            return
+        self.engine.set_option("cross_mode", 0 if rows_per_window > 1 else 1)
+
     def _encode(self, features: torch.Tensor, seek: int, size: int, slot: int = 0) -> torch.Tensor:
         enc = self.engine.encode(features, [seek], [size])
         self.engine.cross_kv(enc, slot)
@@ -464,6 +474,7 @@ class WhisperModel:
             # one lock scope from the encode to the word alignment: the alignment reads the window's encoder
             # output from slot 0, which another thread's transcribe must not replace in between
             with self._lock:
+                self._use_cross_form(options.beam_size)
                 self._encode(features, seek, segment_size, 0)
                 prompt = self.get_prompt(tokenizer, previous_tokens, options.without_timestamps)
                 result, avg_lp, temperature, cr = self.generate_with_fallback(prompt, tokenizer, options, seed=window)
@@ -708,11 +719,9 @@ class BatchedInferencePipeline:
         max_length = min(m.max_length, len(prompt) + options.max_new_tokens) if options.max_new_tokens else m.max_length
         mit = int(round(options.max_initial_timestamp / m.time_precision))
         per = max(options.beam_size, options.best_of, 1)
-        # cross-attention form per batch: the factored form (attention over the encoder output) reads half the
-        # bytes per window and wins for one row per window; with beam / best-of groups the projected K/V form
-        # wins (large-v3, 150 windows, beam 5 + words: 1474 vs 1237 RTFx) because every group's rows share one
-        # K/V stream there, while the factored kernel re-reads E per 32 (row, head) pairs
-        # (opt-in fp8 cross memory is a factored-form mode: the automatic switch never overrides it)
+        # cross-attention form per batch (WhisperModel._use_cross_form), chosen for the FIRST pass: greedy
+        # (beam 1) decodes one row per window -> factored; beam groups -> projected (large-v3, 150 windows, beam 5
+        # + words: 1474 vs 1237 RTFx).  The temperature-fallback passes (best_of rows) reuse the batch's form.
         auto_form = os.environ.get("VLOG_AMD_CROSS_AUTO", "1") != "0" and not eng.option("cross_fp8", 0)
         prev_form = eng.option("cross_mode")
         try:
@@ -734,7 +743,7 @@ class BatchedInferencePipeline:
             wins = list(windows[b0: b0 + B])
             with m._lock:
                 if auto_form:
-                    eng.set_option("cross_mode", 0 if per > 1 else 1)
+                    m._use_cross_form(options.beam_size)
                 eng.reserve(len(wins), len(wins) * per)
                 enc = eng.encode(features, [w[0] for w in wins], [w[1] for w in wins])
                 eng.cross_kv(enc, 0)
