@@ -5,4 +5,4 @@ timeout -k 10 600 python tools/bench_worker_call.py --minutes-seq 2 --minutes-tp
 timeout -k 10 600 python tools/bench_worker_call.py --minutes-seq 2 --minutes-tp 30 --no-graph > gpurun_out/worker_g0.json 2> gpurun_out/worker_g0.err && cat gpurun_out/worker_g0.json &&
 timeout -k 10 600 python bench.py --steps 5 --warmup 1 --no-profile --no-cpu-baseline --no-parity > gpurun_out/bench_g1.json 2>/dev/null && head -c 600 gpurun_out/bench_g1.json && echo &&
 VLOG_AMD_DEC_GRAPH=0 timeout -k 10 600 python bench.py --steps 5 --warmup 1 --no-profile --no-cpu-baseline --no-parity > gpurun_out/bench_g0.json 2>/dev/null && head -c 600 gpurun_out/bench_g0.json &&
-timeout -k 10 900 python tools/bench_product.py --hours 1 10 > gpurun_out/product.json 2> gpurun_out/product.err && cat gpurun_out/product.json
+timeout -k 10 900 python tools/bench_product.py --hours 1 10 > gpurun_out/product.json 2> gpurun_out/product.err && cat gpurun_out/product.json && timeout -k 10 300 python tools/blas_probe.py > gpurun_out/blas_probe.txt 2>&1 && cat gpurun_out/blas_probe.txt
