@@ -16,8 +16,15 @@ from vlog_amd.transcribe import WhisperModel  # noqa: E402
 
 
 def main():
+    # usage: prof_worker_seq.py [model] [opt=value,opt=value]  (engine options, e.g. decode_gemm.qkv=-1)
     model = WhisperModel(f"synthetic:{sys.argv[1] if len(sys.argv) > 1 else 'large-v3'}:0:margin", device="cpu",
                          compute_type="int8")
+    opts = {}
+    if len(sys.argv) > 2 and sys.argv[2]:
+        for kv in sys.argv[2].split(","):
+            k, v = kv.split("=")
+            opts[k] = int(v)
+            model.engine.set_option(k, int(v))
     wav = os.path.join(tempfile.mkdtemp(), "c.wav")
     write_wav(wav, np.concatenate([speech_like(30.0, i) for i in range(2)]))
     list(model.transcribe(wav, beam_size=5)[0])              # warm-up
@@ -28,7 +35,7 @@ def main():
     dt = time.perf_counter() - t
     eng.profile(False)
     prof = {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in eng.profile_read().items() if v["launches"]}
-    print(json.dumps({"wall_s": round(dt, 3), "audio_s": 60.0, "rtfx": round(60.0 / dt, 1), "segments": len(segs),
+    print(json.dumps({"opts": opts, "wall_s": round(dt, 3), "audio_s": 60.0, "rtfx": round(60.0 / dt, 1), "segments": len(segs),
                       "gpu_ms_by_class": prof, "sum_gpu_ms": round(sum(v["ms"] for v in prof.values()), 1)}))
 
 

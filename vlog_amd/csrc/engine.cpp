@@ -166,6 +166,7 @@ struct wm_engine {
   int dec_kr[6] = {0, 0, 0, 0, 0, 0};           // ring GEMM K range per block (0: the whole K up to 1280)
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int dec_graph = 1;         // decode steps replayed from one captured HIP graph (see generate)
+  int dec_gemv = 1;          // passes of <= 32 rows: the small-M weight-streaming GEMM (gemm_dec.hip gemv)
   hipStream_t gst = nullptr; // the capture / replay stream (a graph cannot be captured on the legacy null stream)
   hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr;
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
@@ -512,6 +513,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   auto gemm = [&](int proj, const GemmA& a, const bf16* w, long long ldw, int N, int K, const GemmEpi& ep) {
     const double ob = (ep.kind == EPI_RESID_F32) ? 8 : (ep.kind == EPI_RESID_LN) ? 10 : 2;
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
+    // one window's beam (or a handful of rows): the weight-streaming small-M kernel
+    if (sl.total_rows <= 32 && e->dec_gemv && launch_dec_gemv(a, w, ldw, rows, N, K, ep, ws, wsb, st)) return;
     const int p = plan_of(proj);
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
@@ -547,7 +550,9 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   {
     GemmEpi ep = epi_of(EPI_BF16, q, d, W.cq_b);
     const int pcq = plan_of(DEC_CQ);
-    const int sk = pcq == -1 ? skinny_splits(rows, d, d, wsb)
+    const int gsk = (sl.total_rows <= 32 && e->dec_gemv) ? gemv_splits(rows, d, d, nullptr) : 0;
+    const int sk = gsk > 0 ? gsk
+                 : pcq == -1 ? skinny_splits(rows, d, d, wsb)
                              : (pcq > 0 && e->dec_kr[DEC_CQ] > 0 ? (d + e->dec_kr[DEC_CQ] - 1) / e->dec_kr[DEC_CQ] : 1);
     if ((e->cross_fuse & 1) && !(attn && align_map) && sk > 1) {
       ep.defer_combine = 1;
@@ -1234,6 +1239,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     e->device = device;
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_GRAPH")) e->dec_graph = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_GEMV")) e->dec_gemv = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_PLAN")) {
       const int p = std::atoi(v) != 0;
@@ -1510,6 +1516,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     const std::string k(key);
     if (k == "decode_split") e->dec_split = value != 0;
     else if (k == "decode_graph") e->dec_graph = value != 0;
+    else if (k == "decode_gemv") e->dec_gemv = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
     else if (k == "decode_gemm_plan") {
       if (value != 0 && value != 1) throw std::runtime_error("wm_set_option: decode_gemm_plan is 0 or 1");

@@ -73,3 +73,9 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
 // <= 1280-deep K range issued at once into MFMA operand registers, per-wave K split summed through LDS.
 bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                         size_t ws_bytes, int nc, hipStream_t st);
+// Small-M decoder path (gemm_dec.hip): M <= 32 rows, 16 output columns x a K range per 256-thread block, every
+// weight fragment of the range issued at once (non-temporal), split-K where the tiles alone do not fill the chip.
+// gemv_splits: the split count it would use (0: unsupported), kr_out = K range per block.
+int gemv_splits(int M, int N, int K, int* kr_out);
+bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     size_t ws_bytes, hipStream_t st);

@@ -527,3 +527,120 @@ bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int
   if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
   return true;
 }
+
+// ------------------------------------------------------------------------------------------------------
+// Small-M weight-streaming decoder GEMM (M <= 32 rows: one window's beam, a few windows): at these row counts
+// a projection is a GEMV over the weight matrix, and the cost is how many weight bytes each CU has in
+// flight and how many CUs stream.  One 256-thread block = 16 output columns x a K range of kr (a multiple of
+// 128); wave w owns an equal share of its 32-deep k-steps and issues ALL of them at once: the weight
+// fragments (16 B per lane, non-temporal: each weight byte is read once per step, MI355X_MICROARCH
+// nt-weights) and the activation fragments (rows clamped to M - 1, L2/L1-resident), then its MFMAs
+// (16x16x32: the weight fragment is the A operand, 16 columns x 32 k; the activations the B operand, 32 k x
+// 16 rows, MF fragments of 16 rows).  The 4 wave partials are summed through LDS in wave order, then the
+// epilogue runs in place (or a split-K slab is written: RESID_LN always, other kinds when kr < K).  Grid =
+// 16-column tiles x K splits, >= ~256 blocks (gemv_plan).
+template <int MF, int KSW, int KIND>
+__global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
+                                                       int K, GemmEpi epi, int splitk, int kr, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) f32x4 sred[4][MF][64];
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int split = wgid % splitk, tile = wgid / splitk;
+  const int n0 = tile * 16;
+  const int kb = split * kr, klen = min(kr, K - kb), nks = klen / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int s0 = wv * nks / 4, s1 = (wv + 1) * nks / 4;
+  const bf16* wr = w + (long long)min(n0 + (lane & 15), N - 1) * ldw + kb + 8 * (lane >> 4);
+  const bf16* ar[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const int m = min(i * 16 + (lane & 15), M - 1);
+    const long long off = a.rpb ? (long long)(m / a.rpb) * a.bstride + (long long)(m % a.rpb) * a.ld : (long long)m * a.ld;
+    ar[i] = a.ptr + off + kb + 8 * (lane >> 4);
+  }
+  bf16x8 fw[KSW], fa[KSW][MF];
+#pragma unroll
+  for (int s = 0; s < KSW; ++s) {
+    if (s0 + s < s1) {
+      fw[s] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const i32x4*)(wr + 32 * (s0 + s))));
+#pragma unroll
+      for (int i = 0; i < MF; ++i) fa[s][i] = *(const bf16x8*)(ar[i] + 32 * (s0 + s));
+    }
+  }
+  f32x4 acc[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KSW; ++s)
+    if (s0 + s < s1) {
+#pragma unroll
+      for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[s], fa[s][i], acc[i], 0, 0, 0);
+    }
+#pragma unroll
+  for (int i = 0; i < MF; ++i) sred[wv][i][lane] = acc[i];
+  __syncthreads();
+  if (wv != 0) return;
+  // acc holds C^T: lane l has row m = 16 i + (l & 15) and the 4 consecutive columns n0 + 4 (l >> 4) + e
+  const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
+  const int col0 = n0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const f32x4 v = sred[0][i][lane] + sred[1][i][lane] + sred[2][i][lane] + sred[3][i][lane];
+    const int row = i * 16 + (lane & 15);
+    if (row >= M || col0 >= N) continue;
+    if (to_slab)
+      *(f32x4*)(part + ((long long)split * M + row) * N + col0) = v;
+    else
+      apply_epi4<KIND>(epi, row, col0, v);
+  }
+}
+
+// K range per block for the small-M path: no split when the 16-column tiles alone reach 3/4 of the CUs;
+// otherwise split K (ranges of a multiple of 128, <= 1280) until the grid reaches ~256 blocks.
+int gemv_splits(int M, int N, int K, int* kr_out) {
+  if (M <= 0 || M > 32 || N % 16 != 0 || K % 128 != 0) return 0;
+  const int tiles = N / 16;
+  int s = tiles >= 192 ? 1 : (256 + tiles - 1) / tiles;
+  s = std::max(s, (K + 1279) / 1280);                     // <= 10 k-steps per wave
+  int kr = ((K + s - 1) / s + 127) / 128 * 128;
+  s = (K + kr - 1) / kr;
+  if (kr_out) *kr_out = kr;
+  return s;
+}
+
+template <int MF, int KIND>
+static void run_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     int splitk, int kr, hipStream_t st) {
+  hipLaunchKernelGGL((gemv_dec_kernel<MF, 10, KIND>), dim3((N / 16) * splitk), dim3(256), 0, st, a, w, ldw, M, N, K, epi,
+                     splitk, kr, ws);
+  WM_LAUNCH_CHECK("gemv_dec_kernel");
+}
+
+template <int KIND>
+static void dispatch_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
+                          float* ws, int splitk, int kr, hipStream_t st) {
+  if (M <= 16) run_gemv<1, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_gemv<2, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+}
+
+// Small-M path: M <= 32, N % 16 == 0, K % 128 == 0.  Returns false when unsupported.
+bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     size_t ws_bytes, hipStream_t st) {
+  int kr = 0;
+  const int splitk = gemv_splits(M, N, K, &kr);
+  if (splitk <= 0) return false;
+  const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
+  if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
+  if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
+  switch (epi.kind) {
+    case EPI_BF16: dispatch_gemv<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_RESID_F32: dispatch_gemv<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_F32: dispatch_gemv<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_DEC_QKV: dispatch_gemv<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    case EPI_RESID_LN: dispatch_gemv<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
+    default: return false;
+  }
+  if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
+  return true;
+}
