@@ -169,7 +169,21 @@ def host_cpu() -> dict:
             if line.startswith("model name"):
                 info["model"] = line.split(":", 1)[1].strip()
                 break
+    info["cpu_share"] = cpu_share()
     return info
+
+
+def cpu_share() -> int:
+    """CPUs this process may actually use: the affinity mask, capped by the cgroup-v2 CPU quota (a GPU box grants
+    one process a share of the host, far fewer CPUs than `os.cpu_count()` reports)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def composite_roofline(dims, lengths, steps: int, prompt_len: int, elapsed_per_step: float, windows: int) -> dict:
@@ -233,6 +247,13 @@ def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
     from vlog_amd.weights import round_bf16
 
     st = dims.specials
+    # every CPU this process is granted (all cores): numpy's BLAS threads follow the thread pool size
+    share = cpu_share()
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=share)
+    except ImportError:
+        limiter = None
     orc = OracleWhisper(round_bf16(sd), dims, np.float32)
     x = speech_like(30.0, 0)
     t0 = time.perf_counter()
@@ -246,10 +267,15 @@ def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
     n_steps = max(1, len(r.tokens))
     per_step = (t2 - t1) / n_steps
     per_window = (t1 - t0) + per_step * max(mean_tokens, 1.0)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = share
+    if limiter is not None:
+        from threadpoolctl import threadpool_info
+        threads = max([p.get("num_threads", 0) for p in threadpool_info()] + [1])
+        limiter.unregister()
     hc = host_cpu()
     return {"value": round(30.0 / per_window, 4), "unit": "audio_s/s", "cores": threads, "kind": "port",
             "cpu_model": hc["model"], "host_physical_cores": hc["physical_cores"], "host_logical_cpus": hc["logical_cpus"],
+            "process_cpu_share": hc["cpu_share"],
             "sample": (f"oracle/ numpy fp32 CPU restatement, {dims.name}: one 30 s window log-mel+encoder+cross-KV "
                        f"({t1 - t0:.1f} s) + {n_steps} greedy decoder steps ({per_step:.3f} s/step), extrapolated to "
                        f"{mean_tokens:.1f} tokens/window; faster-whisper CPU baseline unavailable (not installed)")}
