@@ -201,6 +201,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_graph" (default 1): after one eager decode step, wm_generate captures a step (decoder pass +
  *   token selection) as a HIP graph and replays it for the remaining steps (every per-step quantity lives in
  *   device memory).  Bit-identical either way; off while the event profiler is on or with "decode_split".
+ *   "decode_gemv" (default 1): passes of <= 32 decoder rows (one window's beam, a few windows) run every
+ *   projection on the small-M weight-streaming GEMM (gemm_dec.hip gemv_dec_kernel); it agrees with the other
+ *   routes to f32 rounding.
  *   "decode_ring_gemm" (default 1): 0 disables the all-rows ring GEMM (plan value 0 below falls back to the
  *   split-K skinny GEMM).
  *   "decode_gemm_plan" (default 1): preset routing of the six decoder projections (qkv, out, cq, cout, fc1, fc2)

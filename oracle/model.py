@@ -16,14 +16,16 @@ oracle the bf16-rounded weights.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 from scipy.special import erf
 
 
-def to_bf16(x: np.ndarray) -> np.ndarray:
-    """Round float32 values to bfloat16 (round-to-nearest-even) and return them as float32."""
+def to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """Round float32 values to bfloat16 (round-to-nearest-even) and return them as float32 (the definition, in
+    integer arithmetic on the bit pattern)."""
     x32 = np.ascontiguousarray(x, dtype=np.float32)
     u = x32.view(np.uint32)
     # finite values: u <= 0xFF7FFFFF, so u + 0x8000 cannot wrap in uint32
@@ -31,8 +33,55 @@ def to_bf16(x: np.ndarray) -> np.ndarray:
     return np.where(np.isfinite(x32), r, x32)
 
 
-def gelu(x: np.ndarray) -> np.ndarray:
+def to_bf16(x: np.ndarray) -> np.ndarray:
+    """to_bf16_bits, computed by PyTorch's CPU float32 -> bfloat16 conversion (the same round-to-nearest-even,
+    multithreaded: the oracle's bf16-activation mode rounds every activation, and the numpy form was half the
+    oracle's time at large-v3 sizes).  tests/test_oracle_model.py pins the two forms bit for bit."""
+    try:
+        import torch
+    except ImportError:                     # pragma: no cover - torch is part of this image
+        return to_bf16_bits(x)
+    x32 = np.ascontiguousarray(x, dtype=np.float32)
+    return torch.from_numpy(x32).to(torch.bfloat16).float().numpy()
+
+
+_POOL = None
+
+
+def _threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:                  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+def par_rows(fn, *arrays, min_rows: int = 2):
+    """fn applied to slices of the leading axis of `arrays` on a thread pool, results concatenated on axis 0.
+    Only for computations that are independent per leading index (numpy's elementwise ufuncs and batched
+    matmul release the GIL and run single-threaded; the result is identical to fn(*arrays))."""
+    global _POOL
+    n = arrays[0].shape[0]
+    k = min(_threads(), n // max(1, min_rows))
+    if k <= 1:
+        return fn(*arrays)
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max_workers=_threads())
+    cuts = [n * i // k for i in range(k + 1)]
+    parts = list(_POOL.map(lambda i: fn(*(a[cuts[i]:cuts[i + 1]] for a in arrays)), range(k)))
+    if isinstance(parts[0], tuple):
+        return tuple(None if parts[0][j] is None else np.concatenate([p[j] for p in parts], axis=0)
+                     for j in range(len(parts[0])))
+    return np.concatenate(parts, axis=0)
+
+
+def _gelu(x: np.ndarray) -> np.ndarray:
     return 0.5 * x * (1.0 + erf(x / np.sqrt(2.0)).astype(x.dtype))
+
+
+def gelu(x: np.ndarray) -> np.ndarray:
+    return par_rows(_gelu, x) if x.ndim >= 2 and x.size >= (1 << 20) else _gelu(x)
 
 
 def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float = 1e-5) -> np.ndarray:
@@ -104,7 +153,9 @@ class OracleWhisper:
         s = (q @ np.swapaxes(k, -1, -2)) / np.sqrt(self.hd).astype(self.dtype)
         if mask is not None:
             s = s + mask
-        p = softmax(s, -1)
+        # the softmax is elementwise per row: sliced over a thread pool (numpy's ufuncs are single-threaded);
+        # the matmuls stay on the calling thread (BLAS threads itself)
+        p = par_rows(softmax, s) if s.size >= (1 << 20) else softmax(s, -1)
         o = p @ v
         return (o, p) if return_weights else (o, None)
 
@@ -165,11 +216,11 @@ class OracleWhisper:
     # ---------------------------------------------------------------- decoder
     def cross_kv(self, enc: np.ndarray) -> List[Tuple[np.ndarray, np.ndarray]]:
         out = []
-        enc = np.asarray(enc, dtype=self.dtype)
+        enc = self._q(np.asarray(enc, dtype=self.dtype))
         for i in range(self.dims.n_dec_layer):
             p = f"model.decoder.layers.{i}.encoder_attn."
-            k = self._q(self._lin(self._q(enc), p + "k_proj", bias=False))
-            v = self._q(self._lin(self._q(enc), p + "v_proj"))
+            k = self._q(self._lin(enc, p + "k_proj", bias=False))
+            v = self._q(self._lin(enc, p + "v_proj"))
             out.append((self._split(k), self._split(v)))
         return out
 

@@ -59,3 +59,20 @@ def test_bf16_format_modes_stay_within_rounding_noise():
     r = generate_one(bf, cross, prompt, st, opt)
     chosen, best, score, ns = teacher_force(bf, cross, prompt, r.tokens, st, opt, len(prompt) + len(r.tokens) < 60)
     assert np.all(chosen - best >= -1e-9) and abs(score - r.score) < 1e-6 and abs(ns - r.no_speech_prob) < 1e-9
+
+
+def test_bf16_rounding_forms_bit_identical():
+    """oracle.model.to_bf16 (PyTorch's float32 -> bfloat16 conversion, used for speed) equals the integer
+    round-to-nearest-even definition to_bf16_bits bit for bit, ties, subnormals, overflow and non-finite
+    values included."""
+    from oracle.model import to_bf16, to_bf16_bits
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal(200000) * np.exp(rng.uniform(-90, 90, 200000))).astype(np.float32)
+    ties = (rng.integers(0, 1 << 31, 4096, dtype=np.uint32) & np.uint32(0xFFFF0000)) | np.uint32(0x8000)
+    edge = np.array([np.inf, -np.inf, np.nan, 0.0, -0.0, 3.4e38, -3.4e38, 3.3895e38, 1e-45, -1e-45, 1e-40],
+                    dtype=np.float32)
+    x = np.concatenate([x, ties.view(np.float32), edge])
+    a, b = to_bf16(x), to_bf16_bits(x)
+    fin = ~np.isnan(x)
+    assert np.array_equal(a.view(np.uint32)[fin], b.view(np.uint32)[fin])
+    assert np.isnan(a[~fin]).all()

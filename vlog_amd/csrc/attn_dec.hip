@@ -52,6 +52,7 @@ struct DecAttnArgs {
 };
 
 #define CT_MAX 1536
+#define QMAXS 16               // max cq split-K slabs summed in the cross-attention q load
 
 // One 256-thread workgroup per (row, head[, key split]); 4 waves x 8 keys per step, 8 lanes x 16 B per key row.
 // SELF: keys are positions 0..row_pos of the row's hypothesis, each from physical slot lin[hyp][p].
@@ -216,7 +217,7 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
 // LDS.  With splits > 1 the (m, l, o) partials go to cross_combine_kernel (per row, as the legacy path).
 template <int RG>
 __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int split, float (&s_m)[4][RG],
-                                           float (&s_l)[4][RG], float (&s_o)[4][RG][HD]) {
+                                           float (&s_l)[4][RG], float (&s_o)[4][RG][HD], float (&s_q)[RG][HD]) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int sub = lane & 7, g = lane >> 3;
   const int H = a.H;
@@ -240,24 +241,37 @@ __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int spl
     atomicAdd(a.stat + ((bx + split) & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + RG * 2 * HD * 2));
 
   float qf[RG][8];
+  if (a.q_part) {
+    // the cq split-K slabs summed into q by the whole block in ONE memory round trip (every slab load of a
+    // value issued before any add), in slab order plus the bias as splitk_reduce_kernel does (bit-identical
+    // to the unfused bf16 q); the rows go through LDS.  (Per lane and row, a runtime loop over the slabs paid
+    // one dependent round trip per slab and row: ~18 us per launch at 5 rows x 4 slabs.)
+    const long long slab = (long long)a.q_rows * a.ldq;
+    for (int idx = tid; idx < RG * HD; idx += 256) {
+      const int r = idx / HD, e = idx - r * HD;
+      const float* pq = a.q_part + (long long)(row0 + r) * a.ldq + h * HD + e;
+      float pv[QMAXS];
 #pragma unroll
-  for (int r = 0; r < RG; ++r) {
-    if (a.q_part) {
-      const long long slab = (long long)a.q_rows * a.ldq;
-      const float* pq = a.q_part + (long long)(row0 + r) * a.ldq + h * HD + sub * 8;
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int sp = 0; sp < a.q_splits; ++sp) {
-        const f32x4 lo = *(const f32x4*)(pq + sp * slab), hi = *(const f32x4*)(pq + sp * slab + 4);
+      for (int sp = 0; sp < QMAXS; ++sp)
+        if (sp < a.q_splits) pv[sp] = pq[sp * slab];
+      float v = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { v[i] += lo[i]; v[4 + i] += hi[i]; }
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) qf[r][i] = bf2f(f2bf(v[i] + a.q_bias[h * HD + sub * 8 + i]));
-    } else {
-      load8(a.q + (long long)(row0 + r) * a.ldq + h * HD + sub * 8, qf[r]);
+      for (int sp = 0; sp < QMAXS; ++sp)
+        if (sp < a.q_splits) v += pv[sp];
+      s_q[r][e] = bf2f(f2bf(v + a.q_bias[h * HD + e]));
     }
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 8; ++i) qf[r][i] *= a.scale_log2;
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qf[r][i] = s_q[r][sub * 8 + i] * a.scale_log2;
+  } else {
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      load8(a.q + (long long)(row0 + r) * a.ldq + h * HD + sub * 8, qf[r]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qf[r][i] *= a.scale_log2;
+    }
   }
   float m[RG], l[RG], o[RG][8];
 #pragma unroll
@@ -409,8 +423,9 @@ template <int RG>
 __global__ __launch_bounds__(256) void cross_attn_group_kernel(DecAttnArgs a, int n_items) {
   __shared__ float s_m[4][RG], s_l[4][RG];
   __shared__ float s_o[4][RG][HD];
+  __shared__ float s_q[RG][HD];
   for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
-    cross_item<RG>(a, it / a.splits, it % a.splits, s_m, s_l, s_o);
+    cross_item<RG>(a, it / a.splits, it % a.splits, s_m, s_l, s_o, s_q);
     __syncthreads();
   }
 }
@@ -569,6 +584,7 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
                        hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
   if (plan_rows < rows) plan_rows = rows;
+  if (fz.q_part && fz.q_splits > QMAXS) throw std::runtime_error("cross_attn: too many cq split-K slabs");
   DecAttnArgs a{};
   a.q_part = fz.q_part; a.q_splits = fz.q_splits; a.q_rows = fz.q_rows; a.q_bias = fz.q_bias; a.cnt = fz.cnt;
   a.q = q; a.ldq = ldq; a.kbase = kbase; a.vbase = vbase; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
@@ -595,7 +611,9 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
   // result, bit for bit — does not depend on how the pass was sliced into launches.
   const int plan_blocks = plan_rows / rg * H;
   int splits = ((rg == 1 ? 10240 : 2048) + plan_blocks - 1) / plan_blocks;
-  splits = std::max(1, std::min(splits, std::min(16, T / 128)));
+  // at most one 128-key pass per block when the grid is small (a 1500-key window: 12 splits of 125 keys, not
+  // 11 of 137, which took a second, nearly empty pass through the dependent load loop)
+  splits = std::max(1, std::min(splits, std::min(16, (T + 127) / 128)));
   a.splits = splits;
   const int n_items = blocks * splits;
   // events (profiler): start on the attention kernel, stop on the last kernel of the pair

@@ -639,6 +639,11 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
   const auto& m = e->dm;
   const int d = m.n_state, L = m.n_dec_layer;
   const auto& W0 = dec_weights(e)[0];
+  // host-side check of the row buffers against what the launches below index (rows of the pass, and the
+  // final LayerNorm's gathered logit rows)
+  if ((size_t)rows * d * 4 > e->s_x.bytes || (size_t)std::max(rows, n_logit) * d * 2 > e->s_hb.bytes)
+    throw std::runtime_error("decoder_pass: row buffers smaller than the pass (" + std::to_string(rows) + " rows, " +
+                             std::to_string(n_logit) + " logit rows)");
   if (e->cross_mode == 1) {
     // factored cross-attention scratch for the whole pass (slices index it by absolute row), and the
     // per-head Wk^T layout (packed once per upload of dec.ckv.w)
@@ -764,6 +769,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   const int W = a->n_windows, P = a->prompt_len;
   if (W <= 0) return;
   if (P <= 0 || P >= a->max_length || a->max_length > C) throw std::runtime_error("generate: bad prompt_len/max_length");
+  if (a->sot_index >= P) throw std::runtime_error("generate: sot_index outside the prompt");
   const bool beam = a->beam_size > 1 && a->temperature <= 0.f;
   const bool sampling = a->temperature > 0.f;
   const int per = beam ? a->beam_size : (sampling ? std::max(1, a->num_hypotheses) : 1);
@@ -778,11 +784,15 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   // ---- host-side init of the state tables
   std::vector<int> tokens((size_t)NH * C, 0), lin((size_t)NH * C, 0), seq_len(NH, P), zeros(NH, 0), hyp_slot(NH);
   std::vector<float> cum(NH, 0.f);
+  // Beam search: the hypotheses of a window share its prompt, so the prompt is prefilled once per window (into
+  // the first hypothesis' self-KV rows) and every hypothesis' lineage points its prompt positions there (the
+  // lineage is what beam reordering copies; the cache itself is never copied).  Greedy / sampling keep one
+  // prefill per hypothesis: their self-attention reads each row's own cache (no lineage table).
   for (int h = 0; h < NH; ++h) {
     const int w = h / per;
     hyp_slot[h] = a->h_slots[w];
     for (int p = 0; p < P; ++p) tokens[(size_t)h * C + p] = a->h_prompts[(size_t)w * P + p];
-    for (int p = 0; p < C; ++p) lin[(size_t)h * C + p] = h;
+    for (int p = 0; p < C; ++p) lin[(size_t)h * C + p] = (beam && p < P) ? w * per : h;
     if (beam && (h % per) != 0) cum[h] = -INFINITY;
   }
   std::vector<unsigned char> sup(V, 0);
@@ -799,20 +809,25 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   int n_active = NH;
   HIP_OK(hipMemcpyAsync(e->d_n_active.p, &n_active, 4, hipMemcpyHostToDevice, st));
 
-  // ---- prefill: rows (h, p) for every prompt position
-  const int rows = NH * P;
+  // ---- prefill: rows (h, p) for every prompt position of every prefilled hypothesis (beam: one per window)
+  const int pf_per = beam ? per : 1;                 // hypotheses per prefilled row set
+  const int n_pf = NH / pf_per;
+  const int rows = n_pf * P;
   const int nlog = a->sot_index >= 0 ? 2 * NH : NH;
-  ensure_step(e, std::max(rows, NH), std::max(nlog, NH));
+  // the pass's final LayerNorm gathers its nlog logit rows into s_hb rows [0, nlog): with the beam's shared
+  // prefill (rows = W * P) that can exceed the pass rows, so the row buffers hold max(rows, NH, nlog)
+  ensure_step(e, std::max(std::max(rows, NH), nlog), std::max(nlog, NH));
   {
     std::vector<int> rt(rows), rp(rows), rh(rows), lr(nlog);
-    for (int h = 0; h < NH; ++h)
+    for (int i = 0; i < n_pf; ++i)
       for (int p = 0; p < P; ++p) {
-        const int r = h * P + p;
+        const int r = i * P + p, h = i * pf_per;
         rt[r] = tokens[(size_t)h * C + p]; rp[r] = p; rh[r] = h;
       }
-    for (int h = 0; h < NH; ++h) {
-      lr[h] = h * P + P - 1;
-      if (a->sot_index >= 0) lr[NH + h] = h * P + a->sot_index;
+    for (int h = 0; h < NH; ++h) {            // a hypothesis' logits come from its row set's last prompt row
+      const int i = h / pf_per;
+      lr[h] = i * P + P - 1;
+      if (a->sot_index >= 0) lr[NH + h] = i * P + a->sot_index;
     }
     HIP_OK(hipMemcpyAsync(e->d_prow_tok.p, rt.data(), rows * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(e->d_prow_pos.p, rp.data(), rows * 4, hipMemcpyHostToDevice, st));
@@ -825,7 +840,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   }
   float* logits = e->s_logits.as<float>();
   decoder_pass(e, rows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_prow_hyp.as<int>(), nullptr,
-               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, logits, nullptr, 0, nullptr, per * P, st);
+               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, logits, nullptr, 0, nullptr, (per / pf_per) * P, st);
   if (a->sot_index >= 0) launch_no_speech(logits + (size_t)NH * V, V, V, NH, m.no_speech, e->d_ns.as<float>(), st);
 
   SearchParams sp;

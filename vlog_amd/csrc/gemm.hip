@@ -471,6 +471,21 @@ void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int
     return;
   }
   const bool vec4 = epi.ldc % 4 == 0 && (epi.rpb == 0 || epi.bstride % 4 == 0);   // 4-column vector epilogue
+  // large-tile kernels need enough 256 x 256 tiles to occupy the CUs (one window's encoder is 6 row tiles:
+  // 30-120 tiles for 256 CUs); below VLOG_AMD_GEMM_MIN_TILES of them the 128 x 128 kernel runs instead
+  static const int min_tiles = [] {
+    const char* e = std::getenv("VLOG_AMD_GEMM_MIN_TILES");
+    return e ? std::atoi(e) : 0;
+  }();
+  const long long tiles256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  if (tiles256 < min_tiles) {
+    switch (epi.kind) {
+      case EPI_BF16: run<128, 128, 2, 2, EPI_BF16>(a, w, ldw, M, N, K, epi, nullptr, 0, st); return;
+      case EPI_RESID_F32: run<128, 128, 2, 2, EPI_RESID_F32>(a, w, ldw, M, N, K, epi, nullptr, 0, st); return;
+      case EPI_GELU_POS_F32: run<128, 128, 2, 2, EPI_GELU_POS_F32>(a, w, ldw, M, N, K, epi, nullptr, 0, st); return;
+      default: break;
+    }
+  }
   if (p8_enabled && vec4 && gemm_8p_applicable(M, N, K)) {
     launch_gemm_8p(a, w, ldw, M, N, K, epi, st);
     return;

@@ -21,38 +21,6 @@
 struct Cand { float v; int i; };
 __device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) { return v1 > v2 || (v1 == v2 && i1 < i2); }
 
-__device__ __forceinline__ void topk_insert(Cand (&L)[KMAX], int K, float x, int i) {
-  if (!better(x, i, L[K - 1].v, L[K - 1].i)) return;
-  Cand c{x, i};
-#pragma unroll
-  for (int j = 0; j < KMAX; ++j)
-    if (j < K && better(c.v, c.i, L[j].v, L[j].i)) { Cand t = L[j]; L[j] = c; c = t; }
-}
-
-// Wave-level extraction of the K best from every lane's sorted list; lane 0 writes them to dst[0..K).
-__device__ __forceinline__ void wave_topk(Cand (&L)[KMAX], int K, Cand* dst) {
-  const int lane = threadIdx.x & 63;
-  for (int r = 0; r < K; ++r) {
-    Cand best = L[0];
-    int owner = lane;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float v2 = __shfl_xor(best.v, o, 64);
-      const int i2 = __shfl_xor(best.i, o, 64);
-      const int ow2 = __shfl_xor(owner, o, 64);
-      if (better(v2, i2, best.v, best.i) || (v2 == best.v && i2 == best.i && ow2 < owner)) {
-        best.v = v2; best.i = i2; owner = ow2;
-      }
-    }
-    if (lane == 0) dst[r] = best;
-    if (lane == owner) {
-#pragma unroll
-      for (int j = 0; j < KMAX - 1; ++j) L[j] = L[j + 1];
-      L[KMAX - 1] = Cand{-INFINITY, 0x7fffffff};
-    }
-  }
-}
-
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -102,7 +70,7 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   __shared__ Cand sh_c[NW];
   __shared__ float sh_f[NW];
   __shared__ int s_info[4];
-  __shared__ Cand s_top[2][NW * KMAX];
+  __shared__ Cand s_top[NW * KMAX];
   __shared__ int s_last_ts;
   const int h = blockIdx.x, tid = threadIdx.x;
   if (p.done[h]) return;
@@ -151,10 +119,9 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   // The row is loaded ONCE into registers (PER values per thread, every load issued before any is used),
   // masked entries recorded in a bitmask; both passes then run on registers.  (The earlier form looped
   // over the row twice with one dependent global load per iteration: ~90 us per launch of exposed latency.)
-  // Beam (MODE 1) keeps two local top-k lists as well, which with the row would spill: it re-reads the
-  // (L2-resident) row in each pass instead.
+  // Beam (MODE 1) extracts its top-k in a third pass over the same registers, once `forced` is known.
   constexpr int PER = (53248 + SB - 1) / SB;               // vocab <= 53248
-  constexpr bool RES = MODE != 1;
+  constexpr bool RES = true;
   float xv[RES ? PER : 1];
   unsigned long long live = 0;
   auto xat = [&](int k) -> float { return RES ? xv[k] : lg[tid + k * SB]; };
@@ -173,27 +140,28 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   // pass 1: per-segment max / argmax (and Gumbel keys for sampling, local top-k for beam)
   Cand mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
   Cand gt{-INFINITY, 0x7fffffff}, gs{-INFINITY, 0x7fffffff};
-  Cand kt[KMAX], ks[KMAX];
   const int K = MODE == 1 ? p.topk : 0;
-#pragma unroll
-  for (int j = 0; j < KMAX; ++j) { kt[j] = Cand{-INFINITY, 0x7fffffff}; ks[j] = kt[j]; }
+  // (explicit branches, not a reference chosen per element: a `Cand& m = is_ts ? ms : mt` put both in scratch)
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (!((live >> k) & 1)) continue;
     const int i = tid + k * SB;
     const float x = xat(k);
     const bool is_ts = i >= tb;
-    Cand& m = is_ts ? ms : mt;
-    if (better(x, i, m.v, m.i)) { m.v = x; m.i = i; }
+    if (is_ts) {
+      if (better(x, i, ms.v, ms.i)) { ms.v = x; ms.i = i; }
+    } else {
+      if (better(x, i, mt.v, mt.i)) { mt.v = x; mt.i = i; }
+    }
     if (MODE == 2) {
       // the decode step of this hypothesis = tokens it has sampled so far (equal to the host's step counter
       // for every live hypothesis; read from the device so a captured step graph replays unchanged)
       const float key = x * p.inv_temperature + gumbel(p.seed, h, len - p.sample_begin, i);
-      Cand& gg = is_ts ? gs : gt;
-      if (better(key, i, gg.v, gg.i)) { gg.v = key; gg.i = i; }
-    } else if (MODE == 1) {
-      if (is_ts) topk_insert(ks, K, x, i);
-      else topk_insert(kt, K, x, i);
+      if (is_ts) {
+        if (better(key, i, gs.v, gs.i)) { gs.v = key; gs.i = i; }
+      } else {
+        if (better(key, i, gt.v, gt.i)) { gt.v = key; gt.i = i; }
+      }
     }
   }
   mt = block_argmax(mt, sh_c);
@@ -219,34 +187,57 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   else Z = fmaxf(lse_t, lse_s) + log1pf(expf(-fabsf(lse_t - lse_s)));
 
   if (MODE == 1) {
-    // merge local top-k lists: wave-level extraction, then thread 0 merges the per-wave winners
-    const int wv = tid >> 6;
-    wave_topk(kt, K, &s_top[0][wv * KMAX]);
-    wave_topk(ks, K, &s_top[1][wv * KMAX]);
+    // pass 3: the wave's top-K of the allowed set (timestamps only when forced), K rounds of a wave-wide
+    // (max, argmax) over the register-resident row with the winners cleared from an availability mask (no
+    // per-thread candidate list: with one beside the row the kernel spilled, ~155 us per launch); then
+    // thread 0 merges the per-wave winners (cursors in LDS, not in scratch)
+    unsigned long long avail = live;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (forced && tid + k * SB < tb) avail &= ~(1ull << k);
+    const int wv = tid >> 6, lane = tid & 63;
+    for (int r = 0; r < K; ++r) {
+      Cand best{-INFINITY, 0x7fffffff};
+      int bk = -1;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + k * SB;
+        if (((avail >> k) & 1) && better(xat(k), i, best.v, best.i)) { best.v = xat(k); best.i = i; bk = k; }
+      }
+      int owner = lane;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float v2 = __shfl_xor(best.v, o, 64);
+        const int i2 = __shfl_xor(best.i, o, 64);
+        const int ow2 = __shfl_xor(owner, o, 64);
+        if (better(v2, i2, best.v, best.i) || (v2 == best.v && i2 == best.i && ow2 < owner)) {
+          best.v = v2; best.i = i2; owner = ow2;
+        }
+      }
+      if (lane == 0) s_top[wv * KMAX + r] = best;
+      if (lane == owner && bk >= 0) avail &= ~(1ull << bk);
+    }
+    __shared__ int s_ptr[NW];
+    if (tid < NW) s_ptr[tid] = 0;
     __syncthreads();
     if (tid == 0) {
-      int out = 0;
-      int ptr_t[NW], ptr_s[NW];
-      for (int w = 0; w < NW; ++w) { ptr_t[w] = 0; ptr_s[w] = 0; }
       for (int r = 0; r < K; ++r) {
         Cand best{-INFINITY, 0x7fffffff};
-        int bw = -1, bseg = 0;
-        for (int seg = forced ? 1 : 0; seg < 2; ++seg)
-          for (int w = 0; w < NW; ++w) {
-            const int pp = seg ? ptr_s[w] : ptr_t[w];
-            if (pp >= K) continue;
-            const Cand c = s_top[seg][w * KMAX + pp];
-            if (better(c.v, c.i, best.v, best.i)) { best = c; bw = w; bseg = seg; }
-          }
-        if (bw < 0 || best.v == -INFINITY) {
-          p.cand_tok[(long long)h * p.topk + out] = -1;
-          p.cand_lp[(long long)h * p.topk + out] = -INFINITY;
-        } else {
-          if (bseg) ++ptr_s[bw]; else ++ptr_t[bw];
-          p.cand_tok[(long long)h * p.topk + out] = best.i;
-          p.cand_lp[(long long)h * p.topk + out] = best.v - Z;
+        int bw = -1;
+        for (int w = 0; w < NW; ++w) {
+          const int pp = s_ptr[w];
+          if (pp >= K) continue;
+          const Cand c = s_top[w * KMAX + pp];
+          if (better(c.v, c.i, best.v, best.i)) { best = c; bw = w; }
         }
-        ++out;
+        if (bw < 0 || best.v == -INFINITY) {
+          p.cand_tok[(long long)h * p.topk + r] = -1;
+          p.cand_lp[(long long)h * p.topk + r] = -INFINITY;
+        } else {
+          ++s_ptr[bw];
+          p.cand_tok[(long long)h * p.topk + r] = best.i;
+          p.cand_lp[(long long)h * p.topk + r] = best.v - Z;
+        }
       }
     }
     return;
@@ -295,14 +286,24 @@ void launch_logits_select(const SearchParams& p, int n_hyp, hipStream_t st) {
 #define BMAX 8
 #define CMAX 16
 
+// One workgroup per window.  The K x (K+1) candidates are ranked in parallel (rank = number of candidates
+// that precede it in a stable descending sort of (beam, rank)-ordered candidates), and the ranked list lives in
+// LDS, so the one serial walk (live beams / finished list, <= K (K+1) steps) touches no scratch memory; the
+// finished hypotheses' tokens are copied by the whole workgroup.  (The earlier form ran an insertion sort and
+// the copies in thread 0 over scratch arrays: ~0.2 ms per decode step of the sequential beam-5 call.)
 __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
+  constexpr int NC = BMAX * (BMAX + 1);
   __shared__ int s_tok[BMAX][448];
   __shared__ int s_lin[BMAX][448];
+  __shared__ float c_sc[NC], o_sc[NC];
+  __shared__ int c_ok[NC], o_src[NC], o_tk[NC];
   __shared__ int s_par[BMAX], s_new[BMAX];
   __shared__ float s_sc[BMAX];
-  __shared__ int s_nlive, s_len;
+  __shared__ int f_src[CMAX], f_slot[CMAX];
+  __shared__ float f_sc[CMAX];
+  __shared__ int s_nlive, s_nf_new;
   const int w = blockIdx.x, tid = threadIdx.x;
-  const int K = p.beam, h0 = w * K;
+  const int K = p.beam, h0 = w * K, T = K + 1, NK = K * T;
   if (p.done[h0]) return;
   const int len = p.seq_len[h0];
   for (int i = tid; i < K * len; i += blockDim.x) {
@@ -310,46 +311,44 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
     s_tok[b][t] = p.tokens[(long long)(h0 + b) * p.n_ctx + t];
     s_lin[b][t] = p.lin[(long long)(h0 + b) * p.n_ctx + t];
   }
+  // candidate i = (beam j, rank r) in (beam, rank) order
+  float sc_i = -INFINITY;
+  int tk_i = -1;
+  if (tid < NK) {
+    const int j = tid / T;
+    const float c = p.cum[h0 + j];
+    tk_i = p.cand_tok[(long long)h0 * T + tid];
+    const bool ok = c != -INFINITY && tk_i >= 0;
+    if (ok) sc_i = c + p.cand_lp[(long long)h0 * T + tid];
+    c_ok[tid] = ok;
+    c_sc[tid] = sc_i;
+  }
+  __syncthreads();
+  if (tid < NK && c_ok[tid]) {
+    int rank = 0;
+    for (int j = 0; j < NK; ++j)
+      if (c_ok[j] && (c_sc[j] > sc_i || (c_sc[j] == sc_i && j < tid))) ++rank;
+    o_sc[rank] = sc_i; o_src[rank] = tid / T; o_tk[rank] = tk_i;
+  }
+  __syncthreads();
   if (tid == 0) {
-    // candidates in (beam, rank) order, then a stable sort by score
-    float sc[BMAX * (BMAX + 1)];
-    int src[BMAX * (BMAX + 1)], tk[BMAX * (BMAX + 1)];
     int n = 0;
-    const int T = K + 1;
-    for (int j = 0; j < K; ++j) {
-      const float c = p.cum[h0 + j];
-      if (c == -INFINITY) continue;
-      for (int r = 0; r < T; ++r) {
-        const int t = p.cand_tok[(long long)(h0 + j) * T + r];
-        if (t < 0) continue;
-        sc[n] = c + p.cand_lp[(long long)(h0 + j) * T + r]; src[n] = j; tk[n] = t; ++n;
-      }
-    }
-    for (int a = 1; a < n; ++a) {              // insertion sort, stable, descending
-      const float v = sc[a]; const int s = src[a], t = tk[a];
-      int b = a - 1;
-      while (b >= 0 && sc[b] < v) { sc[b + 1] = sc[b]; src[b + 1] = src[b]; tk[b + 1] = tk[b]; --b; }
-      sc[b + 1] = v; src[b + 1] = s; tk[b + 1] = t;
-    }
-    int nlive = 0;
-    int nf = p.n_fin[w];
+    for (int j = 0; j < NK; ++j) n += c_ok[j];
+    int nlive = 0, nf = p.n_fin[w], nnew = 0;
     for (int c = 0; c < n && nlive < K; ++c) {
-      if (tk[c] == p.eot) {
+      if (o_tk[c] == p.eot) {
         if (nf < p.max_cand) {
-          const int b = src[c];
-          int* dst = p.fin_tok + ((long long)w * p.max_cand + nf) * p.n_ctx;
-          for (int t = p.sample_begin; t < len; ++t) dst[t - p.sample_begin] = s_tok[b][t];
-          p.fin_len[w * p.max_cand + nf] = len - p.sample_begin;
-          p.fin_cum[w * p.max_cand + nf] = sc[c];
+          f_src[nnew] = o_src[c]; f_slot[nnew] = nf; f_sc[nnew] = o_sc[c];
+          ++nnew;
           ++nf;
         }
       } else {
-        s_par[nlive] = src[c]; s_new[nlive] = tk[c]; s_sc[nlive] = sc[c]; ++nlive;
+        s_par[nlive] = o_src[c]; s_new[nlive] = o_tk[c]; s_sc[nlive] = o_sc[c]; ++nlive;
       }
     }
     p.n_fin[w] = nf;
     s_nlive = nlive;
-    s_len = len;
+    s_nf_new = nnew;
     const bool fin = nf >= p.max_cand || len + 1 >= p.max_length || nlive == 0;
     if (fin) {
       for (int j = 0; j < K; ++j) p.done[h0 + j] = 1;
@@ -357,6 +356,17 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
     }
   }
   __syncthreads();
+  {
+    const int nnew = s_nf_new, ng = len - p.sample_begin;
+    for (int i = tid; i < nnew * ng; i += blockDim.x) {
+      const int f = i / ng, t = i - f * ng;
+      p.fin_tok[((long long)w * p.max_cand + f_slot[f]) * p.n_ctx + t] = s_tok[f_src[f]][p.sample_begin + t];
+    }
+    if (tid < nnew) {
+      p.fin_len[w * p.max_cand + f_slot[tid]] = ng;
+      p.fin_cum[w * p.max_cand + f_slot[tid]] = f_sc[tid];
+    }
+  }
   const int nlive = s_nlive;
   // write the new beams (beams beyond nlive are marked dead with cum = -inf)
   for (int i = tid; i < K * len; i += blockDim.x) {
