@@ -32,8 +32,9 @@ def setup(request):
     return dims, eng, orc, enc, tok
 
 
-def _gen(eng, enc, tok, ws, beam, gemv):
+def _gen(eng, enc, tok, ws, beam, gemv, gemv_ln=1):
     eng.set_option("decode_gemv", gemv)
+    eng.set_option("decode_gemv_ln", gemv_ln)
     eng.set_option("cross_mode", 0 if beam > 1 else 1)
     try:
         eng.reserve(enc.shape[0], enc.shape[0] * beam)
@@ -42,6 +43,7 @@ def _gen(eng, enc, tok, ws, beam, gemv):
                               suppress_tokens=list(tok.suppressed_tokens([-1])), max_length=448)
     finally:
         eng.set_option("decode_gemv", 1)
+        eng.set_option("decode_gemv_ln", 1)
         eng.set_option("cross_mode", 1)
     return res
 
@@ -51,7 +53,10 @@ def test_gemv_route_vs_oracle_and_general_route(setup, ws, beam):
     dims, eng, orc, enc, tok = setup
     a = _gen(eng, enc, tok, ws, beam, 1)
     b = _gen(eng, enc, tok, ws, beam, 0)
-    assert [r.tokens for r in a] == [r.tokens for r in b]
+    c = _gen(eng, enc, tok, ws, beam, 1, gemv_ln=0)        # LayerNorm combine launches instead of the fused form
+    assert [r.tokens for r in a] == [r.tokens for r in b] == [r.tokens for r in c]
+    # the fused LayerNorm's statistics are summed in another order (single-pass variance): f32-rounding agreement
+    assert max(abs(x.score - y.score) for x, y in zip(a, c)) < 2e-3
     encf = enc.float().cpu().numpy()
     opt = GenerateOptions(beam_size=beam, suppress_tokens=list(tok.suppressed_tokens([-1])), max_length=448)
     res = {w: r for w, r in zip(ws, a)}

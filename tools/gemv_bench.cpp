@@ -1,0 +1,134 @@
+// Small-M decoder GEMM microbenchmark (tools only; not part of the product): large-v3's per-layer decoder
+// projections at M = 5 / 8 / 16 rows (one window's beam, a few windows) on the small-M path (launch_dec_gemv,
+// + its split-K combine), timed back to back with HIP events (8 rotating weight copies so the stream comes from
+// HBM, not the 256 MB Infinity Cache), against two floors: an empty-kernel chain (the kernel boundary) and a
+// pure weight stream of the same bytes on the same grid.  The target grid size is swept.
+//   usage: gemv_bench [reps]
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+#include "../vlog_amd/csrc/gemm.h"
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                                  \
+    }                                                                                \
+  } while (0)
+
+__global__ void empty_kernel(int x) {
+  if (x == 12345) asm volatile("s_nop 0");
+}
+
+// pure weight stream: block b reads rows [16 (b / s), +16) x K range (b % s) of W, 16-B non-temporal loads all
+// issued before use (the gemv kernel's load pattern without the math)
+__global__ __launch_bounds__(256) void wstream_kernel(const bf16* __restrict__ w, int N, int K, int kr, int splitk,
+                                                      unsigned* sink) {
+  const int tile = blockIdx.x / splitk, split = blockIdx.x % splitk;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int kb = split * kr, nks = min(kr, K - kb) / 32;
+  const int s0 = wv * nks / 4, s1 = (wv + 1) * nks / 4;
+  const bf16* p = w + (long long)(tile * 16 + (lane & 15)) * K + kb + 8 * (lane >> 4);
+  i32x4 v[10];
+#pragma unroll
+  for (int s = 0; s < 10; ++s)
+    if (s0 + s < s1) v[s] = __builtin_nontemporal_load((const i32x4*)(p + 32 * (s0 + s)));
+  unsigned x = 0;
+#pragma unroll
+  for (int s = 0; s < 10; ++s)
+    if (s0 + s < s1) x ^= v[s][0] ^ v[s][1] ^ v[s][2] ^ v[s][3];
+  if (x == 0x9e3779b9u) sink[0] = x;
+}
+
+struct Shape {
+  const char* name;
+  int N, K, kind;
+};
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? std::atoi(argv[1]) : 300;
+  const Shape shapes[] = {{"qkv ", 3840, 1280, EPI_BF16}, {"out ", 1280, 1280, EPI_RESID_LN}, {"cq  ", 1280, 1280, EPI_BF16},
+                          {"fc1 ", 5120, 1280, EPI_BF16}, {"fc2 ", 1280, 5120, EPI_RESID_LN}};
+  size_t maxW = 0;
+  for (auto& s : shapes) maxW = std::max(maxW, (size_t)s.N * s.K);
+  const int MMAX = 32;
+  const size_t maxA = (size_t)MMAX * 5120;
+  std::mt19937 rng(1);
+  std::uniform_real_distribution<float> U(-1.f, 1.f);
+  std::vector<float> hx((size_t)MMAX * 1280), hg(1280, 1.f), hb(1280, 0.f);
+  for (auto& v : hx) v = U(rng);
+  const int NCOPY = 8;
+  bf16 *dA, *dW, *dC, *dLn;
+  float *ws, *dX, *dG, *dB;
+  unsigned* sink;
+  const size_t wsb = 64ull << 20;
+  CK(hipMalloc(&dA, maxA * 2));
+  CK(hipMemset(dA, 0x3c, maxA * 2));
+  CK(hipMalloc(&dW, maxW * 2 * NCOPY));
+  CK(hipMemset(dW, 0x3c, maxW * 2 * NCOPY));
+  CK(hipMalloc(&dC, (size_t)MMAX * 5120 * 2));
+  CK(hipMalloc(&dLn, (size_t)MMAX * 1280 * 2));
+  CK(hipMalloc(&dX, (size_t)MMAX * 1280 * 4));
+  CK(hipMalloc(&dG, 1280 * 4));
+  CK(hipMalloc(&dB, 1280 * 4));
+  CK(hipMemcpy(dX, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dG, hg.data(), 1280 * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dB, hb.data(), 1280 * 4, hipMemcpyHostToDevice));
+  CK(hipMalloc(&ws, wsb));
+  CK(hipMalloc(&sink, 16));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto timeit = [&](auto&& fn) {
+    for (int r = 0; r < 5; ++r) fn(r);
+    CK(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; ++r) fn(r);
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return 1000.0 * ms / reps;
+  };
+  std::printf("empty kernel chain (320 x 256)       %7.2f us\n",
+              timeit([&](int) { hipLaunchKernelGGL(empty_kernel, dim3(320), dim3(256), 0, st, 0); }));
+  for (int M : {5, 16}) {
+    for (int target : {64, 128, 256}) {
+      gemv_set_target_blocks(target);
+      double tot = 0;
+      for (auto& s : shapes) {
+        GemmEpi ep;
+        std::memset(&ep, 0, sizeof(ep));
+        ep.kind = s.kind;
+        if (s.kind == EPI_RESID_LN) {
+          ep.out = dX; ep.ldc = 1280; ep.ln_g = dG; ep.ln_b = dB; ep.ln_out = dLn; ep.ln_ld = 1280;
+        } else {
+          ep.out = dC; ep.ldc = s.N;
+        }
+        const GemmA a{dA, (long long)s.K, 0, 0};
+        int kr = 0;
+        const int sk = gemv_splits(M, s.N, s.K, &kr);
+        const double us = timeit([&](int r) {
+          if (!launch_dec_gemv(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, st)) std::exit(2);
+        });
+        const double fl = timeit([&](int r) {
+          hipLaunchKernelGGL(wstream_kernel, dim3(s.N / 16 * sk), dim3(256), 0, st, dW + maxW * (r % NCOPY), s.N, s.K, kr, sk,
+                             sink);
+        });
+        tot += us;
+        std::printf("M=%2d target %4d %s N=%5d K=%5d splits %2d (%4d blocks)  gemv%s %6.2f us  %6.0f GB/s | W stream %6.2f us\n",
+                    M, target, s.name, s.N, s.K, sk, s.N / 16 * sk, s.kind == EPI_RESID_LN ? "+LN" : "   ", us,
+                    2.0 * s.N * s.K / us / 1e3, fl);
+      }
+      std::printf("M=%2d target %4d  chain of the five: %.2f us\n", M, target, tot);
+    }
+  }
+  return 0;
+}

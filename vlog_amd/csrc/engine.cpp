@@ -32,7 +32,7 @@ void launch_ordered_to_float(const unsigned int*, float*, hipStream_t);
 void launch_frame_energy(const float*, long long, int, int, float*, hipStream_t);
 void launch_pcm_s16(const short*, long long, float*, hipStream_t);
 void launch_layernorm(const float*, long long, const int*, int, int, const float*, const float*, bf16*, long long, hipStream_t);
-void launch_embed(const int*, const int*, const bf16*, const float*, float*, int, int, hipStream_t);
+void launch_embed(const int*, const int*, const bf16*, const float*, float*, int, int, int, int, hipStream_t);
 void launch_im2col_conv1(const float*, long long, const int*, const int*, int, int, int, bf16*, hipStream_t);
 void launch_zero_pad_rows(bf16*, int, long long, int, hipStream_t);
 void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
@@ -167,6 +167,8 @@ struct wm_engine {
   bool dec_split = false;    // two-stream row slices (see decoder_pass)
   int dec_graph = 1;         // decode steps replayed from one captured HIP graph (see generate)
   int dec_gemv = 1;          // passes of <= 32 rows: the small-M weight-streaming GEMM (gemm_dec.hip gemv)
+  int dec_gemv_ln = 1;       // passes of <= 16 rows: the LayerNorms after out / cout computed inside cq / fc1
+  DevBuf d_lnstat;           // their per-(tile, row) partial row sums, one region per decode slice
   hipStream_t gst = nullptr; // the capture / replay stream (a graph cannot be captured on the legacy null stream)
   hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr;
   int cross_fuse = 1;        // bit 0: cq split-K combine, bit 1: key-split combine (last arriver), folded into
@@ -515,6 +517,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
     // one window's beam (or a handful of rows): the weight-streaming small-M kernel
     if (sl.total_rows <= 32 && e->dec_gemv && launch_dec_gemv(a, w, ldw, rows, N, K, ep, ws, wsb, st)) return;
+    if (a.lnx || ep.stat_out) throw std::runtime_error("decoder: fused LayerNorm operand off the small-M path");
     const int p = plan_of(proj);
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
@@ -531,6 +534,24 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     ep.ln_g = g; ep.ln_b = b; ep.ln_out = hb; ep.ln_ld = d;
     return ep;
   };
+  // <= 16 rows: the LayerNorms after out and cout run inside their consumers (cq, fc1), from the residual and
+  // the per-(16-column tile, row) sums their producers write (two combine launches fewer per layer)
+  const bool ln_fuse = sl.total_rows <= 16 && e->dec_gemv && e->dec_gemv_ln && gemv_ln_fusable(rows, d, d, d);
+  float* lnstat = nullptr;
+  if (ln_fuse) {
+    e->d_lnstat.ensure(2 * 128 * 16 * 2 * 4);
+    lnstat = e->d_lnstat.as<float>() + (r0 == 0 ? 0 : 128 * 16 * 2);
+  }
+  auto resid_stat = [&](const float* bias) {
+    GemmEpi ep = epi_of(EPI_RESID_F32, x, d, bias);
+    ep.stat_out = lnstat;
+    return ep;
+  };
+  auto ln_operand = [&](const float* g, const float* b) {
+    GemmA a = amat(nullptr, d);
+    a.lnx = x; a.ln_g = g; a.ln_b = b; a.ln_stat = lnstat; a.ln_tiles = d / 16;
+    return a;
+  };
   bf16* kc = skv + (size_t)(2 * l) * skv_layer;
   bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
   {
@@ -543,7 +564,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
     launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
   }
-  gemm(DEC_OUT, amat(ao, d), W.out_w, d, d, d, resid_ln(W.ln2_w, W.ln2_b, W.out_b));
+  gemm(DEC_OUT, amat(ao, d), W.out_w, d, d, d, ln_fuse ? resid_stat(W.out_b) : resid_ln(W.ln2_w, W.ln2_b, W.out_b));
   // cq: when the skinny split-K path runs it and no attention is captured, its slabs stay in the scratch and
   // the cross-attention kernel sums them while loading q (no combine launch)
   CrossFuse fz;
@@ -558,7 +579,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
       ep.defer_combine = 1;
       fz.q_part = ws; fz.q_splits = sk; fz.q_rows = rows; fz.q_bias = W.cq_b;
     }
-    gemm(DEC_CQ, amat(hb, d), W.cq_w, d, d, d, ep);
+    gemm(DEC_CQ, ln_fuse ? ln_operand(W.ln2_w, W.ln2_b) : amat(hb, d), W.cq_w, d, d, d, ep);
   }
   if ((e->cross_fuse & 2) && e->cross_mode == 0) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   float* probs = nullptr;
@@ -607,11 +628,11 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
                       e->cross_cap, fz, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
   }
   if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
-  gemm(DEC_COUT, amat(ao, d), W.cout_w, d, d, d, resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
+  gemm(DEC_COUT, amat(ao, d), W.cout_w, d, d, d, ln_fuse ? resid_stat(W.cout_b) : resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
   {
     GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, W.fc1_b);
     ep.act = 1;
-    gemm(DEC_FC1, amat(hb, d), W.fc1_w, d, 4 * d, d, ep);
+    gemm(DEC_FC1, ln_fuse ? ln_operand(W.ln3_w, W.ln3_b) : amat(hb, d), W.fc1_w, d, 4 * d, d, ep);
   }
   if (l + 1 < L) {
     const auto& Wn = dec_weights(e)[l + 1];
@@ -684,7 +705,8 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
   for (const auto& s : sl) {
     ProfScope ps(e, P_DEC_OTHER, s.st);
     float* x = e->s_x.as<float>() + (size_t)s.r0 * d;
-    launch_embed(row_tok + s.r0, row_pos + s.r0, e->Wb("dec.embed"), e->Wf("dec.pos"), x, s.rows, d, s.st);
+    launch_embed(row_tok + s.r0, row_pos + s.r0, e->Wb("dec.embed"), e->Wf("dec.pos"), x, s.rows, d, m.n_vocab, m.n_text_ctx,
+                 s.st);
     launch_layernorm(x, d, nullptr, s.rows, d, W0.ln1_w, W0.ln1_b, e->s_hb.as<bf16>() + (size_t)s.r0 * d, d, s.st);
   }
   for (int l = 0; l < L; ++l) {
@@ -1255,6 +1277,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_DEC_SPLIT")) e->dec_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_GRAPH")) e->dec_graph = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_GEMV")) e->dec_gemv = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_GEMV_LN")) e->dec_gemv_ln = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_PLAN")) {
       const int p = std::atoi(v) != 0;
@@ -1309,7 +1332,7 @@ void wm_destroy(wm_engine* e) {
                     &e->d_row_pos, &e->d_row_hyp, &e->d_hyp_slot, &e->d_n_active, &e->d_suppress, &e->d_cand_tok,
                     &e->d_cand_lp, &e->d_fin_tok, &e->d_fin_len, &e->d_fin_cum, &e->d_n_fin, &e->d_ns,
                     &e->d_logit_rows, &e->d_prow_tok, &e->d_prow_pos, &e->d_prow_hyp, &e->d_head_map, &e->s_x,
-                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt,
+                    &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt, &e->d_lnstat,
                     &e->xenc, &e->xscale, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml, &e->a_logits, &e->a_attn,
                     &e->a_next, &e->a_probs, &e->a_rowsum, &e->a_z, &e->a_mat, &e->a_cost, &e->a_trace, &e->a_pi,
                     &e->a_pj, &e->a_plen, &e->a_meta})
@@ -1532,6 +1555,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     if (k == "decode_split") e->dec_split = value != 0;
     else if (k == "decode_graph") e->dec_graph = value != 0;
     else if (k == "decode_gemv") e->dec_gemv = value != 0;
+    else if (k == "decode_gemv_ln") e->dec_gemv_ln = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
     else if (k == "decode_gemm_plan") {
       if (value != 0 && value != 1) throw std::runtime_error("wm_set_option: decode_gemm_plan is 0 or 1");

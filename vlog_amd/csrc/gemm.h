@@ -7,6 +7,14 @@ struct GemmA {
   long long ld;        // elements between consecutive rows
   int rpb;             // rows per batch (0: plain 2-D)
   long long bstride;   // elements between batches
+  // small-M path only (launch_dec_gemv, M <= 16): the operand is LayerNorm(lnx) rounded to bf16, computed in the
+  // kernel from the f32 rows lnx (row stride ld), the affine ln_g / ln_b and the row statistics summed from the
+  // producing GEMM's per-(16-column tile, row) partial sums ln_stat [ln_tiles][M][2] (GemmEpi.stat_out)
+  const float* lnx;
+  const float* ln_g;
+  const float* ln_b;
+  const float* ln_stat;
+  int ln_tiles;
 };
 
 // Epilogue kinds (see gemm.hip for the exact formulas)
@@ -41,6 +49,9 @@ struct GemmEpi {
   // skinny split-K path only: leave the partial slabs in the scratch (no combine launch) for a consumer
   // that sums them itself (see skinny_splits)
   int defer_combine;
+  // small-M path only, EPI_RESID_F32 without split-K: per (16-column tile, row) sums of the updated residual
+  // (sum x, sum x^2) [N/16][M][2] for a LayerNorm-consuming GEMM (GemmA.lnx)
+  float* stat_out;
 };
 
 // Split count the skinny path would use for this shape (>= 1), or 0 when launch_gemm would not take it.
@@ -77,5 +88,9 @@ bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int
 // weight fragment of the range issued at once (non-temporal), split-K where the tiles alone do not fill the chip.
 // gemv_splits: the split count it would use (0: unsupported), kr_out = K range per block.
 int gemv_splits(int M, int N, int K, int* kr_out);
+void gemv_set_target_blocks(int blocks);   // microbenchmark knob (default 256)
 bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      size_t ws_bytes, hipStream_t st);
+// Whether the small-M path can run this shape as a residual producer with row statistics (EPI_RESID_F32 +
+// stat_out, no split-K) and as a LayerNorm-consuming GEMM (GemmA.lnx).
+bool gemv_ln_fusable(int M, int N_prod, int K_prod, int K_cons);

@@ -428,7 +428,10 @@ __global__ __launch_bounds__(512) void dec_oneshot_kernel(GemmA a, const bf16* _
   const int split = wgid % splitk, rg = (wgid / splitk) % rgroups, tile = wgid / (splitk * rgroups);
   const int n0 = tile * (NC * 16), m0 = rg * 32;
   const int kb = split * kr, klen = min(kr, K - kb);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // the wave index through readfirstlane: the k-step guards below are then scalar (wave-uniform) branches.
+  // MFMAs ignore EXEC, so an MFMA behind a guard the compiler treats as divergent would still run, on the
+  // (uninitialised) operand registers of a skipped step (tools/gemv_check found NaN outputs that way)
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nks = klen / 32;                                    // k-steps of this block
   const int s0 = wv * nks / 8, s1 = (wv + 1) * nks / 8;         // this wave's k-steps [s0, s1)
   const int kl = kb + 8 * (lane >> 4);
@@ -539,7 +542,7 @@ bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int
 // 16 rows, MF fragments of 16 rows).  The 4 wave partials are summed through LDS in wave order, then the
 // epilogue runs in place (or a split-K slab is written: RESID_LN always, other kinds when kr < K).  Grid =
 // 16-column tiles x K splits, >= ~256 blocks (gemv_plan).
-template <int MF, int KSW, int KIND>
+template <int MF, int KSW, int KIND, bool LNA>
 __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
                                                        int K, GemmEpi epi, int splitk, int kr, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) f32x4 sred[4][MF][64];
@@ -549,24 +552,98 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
   const int split = wgid % splitk, tile = wgid / splitk;
   const int n0 = tile * 16;
   const int kb = split * kr, klen = min(kr, K - kb), nks = klen / 32;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // wave index through readfirstlane: the k-step guards are scalar branches (MFMAs ignore EXEC, so an MFMA behind a
+  // guard the compiler treats as divergent runs anyway, on a skipped step's uninitialised operands: NaN outputs,
+  // found by tools/gemv_check).  (Zeroing the operands instead costs a memory wait at the first guarded load.)
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = wv * nks / 4, s1 = (wv + 1) * nks / 4;
   const bf16* wr = w + (long long)min(n0 + (lane & 15), N - 1) * ldw + kb + 8 * (lane >> 4);
-  const bf16* ar[MF];
-#pragma unroll
-  for (int i = 0; i < MF; ++i) {
-    const int m = min(i * 16 + (lane & 15), M - 1);
-    const long long off = a.rpb ? (long long)(m / a.rpb) * a.bstride + (long long)(m % a.rpb) * a.ld : (long long)m * a.ld;
-    ar[i] = a.ptr + off + kb + 8 * (lane >> 4);
-  }
   bf16x8 fw[KSW], fa[KSW][MF];
 #pragma unroll
-  for (int s = 0; s < KSW; ++s) {
-    if (s0 + s < s1) {
-      fw[s] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const i32x4*)(wr + 32 * (s0 + s))));
+  for (int s = 0; s < KSW; ++s)
+    if (s0 + s < s1) fw[s] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const i32x4*)(wr + 32 * (s0 + s))));
+  if constexpr (!LNA) {
+    const bf16* ar[MF];
 #pragma unroll
-      for (int i = 0; i < MF; ++i) fa[s][i] = *(const bf16x8*)(ar[i] + 32 * (s0 + s));
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(i * 16 + (lane & 15), M - 1);
+      const long long off = a.rpb ? (long long)(m / a.rpb) * a.bstride + (long long)(m % a.rpb) * a.ld : (long long)m * a.ld;
+      ar[i] = a.ptr + off + kb + 8 * (lane >> 4);
     }
+#pragma unroll
+    for (int s = 0; s < KSW; ++s)
+      if (s0 + s < s1) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) fa[s][i] = *(const bf16x8*)(ar[i] + 32 * (s0 + s));
+      }
+  } else {
+    // LayerNorm-consuming operand (MF == 1: M <= 16).  Issued together with the weight stream: this wave's f32
+    // activation chunks, the block's affine range (into LDS) and the producer's partial row sums; then
+    // A = bf16((x - mean) * rstd * g + b), the arithmetic of resid_ln_reduce_kernel's output.
+    __shared__ __attribute__((aligned(16))) float sg[1280], sb[1280];
+    const int m = min(lane & 15, M - 1);
+    const float* xr = a.lnx + (long long)m * a.ld + kb + 8 * (lane >> 4);
+    f32x4 xv[KSW][2];
+#pragma unroll
+    for (int s = 0; s < KSW; ++s)
+      if (s0 + s < s1) {
+        xv[s][0] = *(const f32x4*)(xr + 32 * (s0 + s));
+        xv[s][1] = *(const f32x4*)(xr + 32 * (s0 + s) + 4);
+      }
+    // every load first (one memory round trip with the weight stream): the block's affine range and this
+    // thread's share of the row statistics -- thread t sums tiles [g T / 16, (g + 1) T / 16) of row t & 15
+    // (g = t >> 4, at most 8 tiles); the 16 group partials go through LDS and each lane adds them in group order
+    // (so every lane of a row, and every block, gets the same bits)
+    __shared__ float sst[16][16][2];
+    constexpr int TG = 8;                                    // T <= 128 tiles (N <= 2048)
+    const int T = a.ln_tiles, g = tid >> 4, r16 = tid & 15, mr = min(r16, M - 1);
+    const int t0 = g * T / 16, t1 = (g + 1) * T / 16;
+    float2 sv[TG];
+#pragma unroll
+    for (int j = 0; j < TG; ++j) sv[j] = *(const float2*)(a.ln_stat + ((long long)min(t0 + j, T - 1) * M + mr) * 2);
+    float gv[5], bv[5];                                      // klen <= 1280 = 5 x 256
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int i = min(tid + 256 * j, klen - 1);
+      gv[j] = a.ln_g[kb + i];
+      bv[j] = a.ln_b[kb + i];
+    }
+    {
+      float q1 = 0.f, q2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < TG; ++j)
+        if (t0 + j < t1) { q1 += sv[j].x; q2 += sv[j].y; }
+      sst[g][r16][0] = q1;
+      sst[g][r16][1] = q2;
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      if (tid + 256 * j < klen) {
+        sg[tid + 256 * j] = gv[j];
+        sb[tid + 256 * j] = bv[j];
+      }
+    __syncthreads();
+    float p1 = 0.f, p2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      p1 += sst[g][lane & 15][0];
+      p2 += sst[g][lane & 15][1];
+    }
+    const float invn = 1.0f / (float)(a.ln_tiles * 16);
+    const float mean = p1 * invn;
+    const float rstd = rsqrtf(fmaxf(p2 * invn - mean * mean, 0.f) + 1e-5f);
+#pragma unroll
+    for (int s = 0; s < KSW; ++s)
+      if (s0 + s < s1) {
+        const int k0 = 32 * (s0 + s) + 8 * (lane >> 4);
+        const f32x4 g0 = *(const f32x4*)(sg + k0), g1 = *(const f32x4*)(sg + k0 + 4);
+        const f32x4 b0 = *(const f32x4*)(sb + k0), b1 = *(const f32x4*)(sb + k0 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          fa[s][0][e] = f2bf((xv[s][0][e] - mean) * rstd * g0[e] + b0[e]);
+          fa[s][0][4 + e] = f2bf((xv[s][1][e] - mean) * rstd * g1[e] + b1[e]);
+        }
+      }
   }
   f32x4 acc[MF];
 #pragma unroll
@@ -584,6 +661,32 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
   // acc holds C^T: lane l has row m = 16 i + (l & 15) and the 4 consecutive columns n0 + 4 (l >> 4) + e
   const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
   const int col0 = n0 + 4 * (lane >> 4);
+  if (KIND == EPI_RESID_F32 && epi.stat_out) {
+    // residual producer for a LayerNorm-consuming GEMM (no split-K): x += acc + bias in place, and this tile's
+    // partial row sums of the new x (columns summed in a fixed order: the 4 of a lane, then the 4 lanes)
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const f32x4 v = sred[0][i][lane] + sred[1][i][lane] + sred[2][i][lane] + sred[3][i][lane];
+      const int row = i * 16 + (lane & 15);
+      const bool ok = row < M && col0 < N;
+      float q1 = 0.f, q2 = 0.f;
+      if (ok) {
+        f32x4 u = v;
+        if (epi.bias) u += *(const f32x4*)(epi.bias + col0);
+        f32x4* xp = (f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0);
+        const f32x4 xn = *xp + u;
+        *xp = xn;
+        q1 = (xn[0] + xn[1]) + (xn[2] + xn[3]);
+        q2 = (xn[0] * xn[0] + xn[1] * xn[1]) + (xn[2] * xn[2] + xn[3] * xn[3]);
+      }
+      q1 += __shfl_xor(q1, 16, 64);
+      q2 += __shfl_xor(q2, 16, 64);
+      q1 += __shfl_xor(q1, 32, 64);
+      q2 += __shfl_xor(q2, 32, 64);
+      if (ok && lane < 16) *(float2*)(epi.stat_out + ((long long)tile * M + row) * 2) = make_float2(q1, q2);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
     const f32x4 v = sred[0][i][lane] + sred[1][i][lane] + sred[2][i][lane] + sred[3][i][lane];
@@ -598,10 +701,13 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
 
 // K range per block for the small-M path: no split when the 16-column tiles alone reach 3/4 of the CUs;
 // otherwise split K (ranges of a multiple of 128, <= 1280) until the grid reaches ~256 blocks.
+static int g_gemv_blocks = 256;          // target grid (tools/gemv_bench sweeps it: gemv_set_target_blocks)
+void gemv_set_target_blocks(int b) { g_gemv_blocks = b > 0 ? b : 256; }
+
 int gemv_splits(int M, int N, int K, int* kr_out) {
   if (M <= 0 || M > 32 || N % 16 != 0 || K % 128 != 0) return 0;
   const int tiles = N / 16;
-  int s = tiles >= 192 ? 1 : (256 + tiles - 1) / tiles;
+  int s = tiles >= (3 * g_gemv_blocks) / 4 ? 1 : (g_gemv_blocks + tiles - 1) / tiles;
   s = std::max(s, (K + 1279) / 1280);                     // <= 10 k-steps per wave
   int kr = ((K + s - 1) / s + 127) / 128 * 128;
   s = (K + kr - 1) / kr;
@@ -609,11 +715,11 @@ int gemv_splits(int M, int N, int K, int* kr_out) {
   return s;
 }
 
-template <int MF, int KIND>
+template <int MF, int KIND, bool LNA = false>
 static void run_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      int splitk, int kr, hipStream_t st) {
-  hipLaunchKernelGGL((gemv_dec_kernel<MF, 10, KIND>), dim3((N / 16) * splitk), dim3(256), 0, st, a, w, ldw, M, N, K, epi,
-                     splitk, kr, ws);
+  hipLaunchKernelGGL((gemv_dec_kernel<MF, 10, KIND, LNA>), dim3((N / 16) * splitk), dim3(256), 0, st, a, w, ldw, M, N, K,
+                     epi, splitk, kr, ws);
   WM_LAUNCH_CHECK("gemv_dec_kernel");
 }
 
@@ -624,15 +730,38 @@ static void dispatch_gemv(const GemmA& a, const bf16* w, long long ldw, int M, i
   else run_gemv<2, KIND>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
-// Small-M path: M <= 32, N % 16 == 0, K % 128 == 0.  Returns false when unsupported.
+bool gemv_ln_fusable(int M, int N_prod, int K_prod, int K_cons) {
+  return M >= 1 && M <= 16 && N_prod % 16 == 0 && N_prod / 16 <= 128 && K_prod % 128 == 0 && K_prod <= 1280 &&
+         K_cons == N_prod && K_cons % 128 == 0;
+}
+
+// Small-M path: M <= 32, N % 16 == 0, K % 128 == 0.  Returns false when unsupported.  A residual producer with
+// row statistics (EPI_RESID_F32 + stat_out) runs without split-K; a LayerNorm-consuming operand (a.lnx) is
+// supported for bf16 outputs at M <= 16.
 bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      size_t ws_bytes, hipStream_t st) {
   int kr = 0;
-  const int splitk = gemv_splits(M, N, K, &kr);
+  int splitk = gemv_splits(M, N, K, &kr);
   if (splitk <= 0) return false;
+  const bool stat = epi.kind == EPI_RESID_F32 && epi.stat_out;
+  if (stat) {
+    if (M > 16 || K > 1280 || N / 16 > 128) return false;
+    splitk = 1;
+    kr = K;
+  }
+  if (a.lnx) {
+    if (epi.kind != EPI_BF16 || M > 16 || kr > 1280 || a.ln_tiles < 1 || a.ln_tiles > 128 || a.ld % 4 != 0 ||
+        a.ln_tiles * 16 != K)
+      return false;
+  }
   const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
+  if (a.lnx) {
+    run_gemv<1, EPI_BF16, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
+    return true;
+  }
   switch (epi.kind) {
     case EPI_BF16: dispatch_gemv<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;
     case EPI_RESID_F32: dispatch_gemv<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st); break;

@@ -66,16 +66,19 @@ void launch_layernorm(const float* x, long long ldx, const int* row_idx, int row
 }
 
 // x[r, :] = E[tok[r], :] + P[pos[r], :]
+// Token ids and positions are clamped to the tables: a numerically broken step (NaN logits select no valid
+// token) then yields a wrong decode that the host reports, never an out-of-bounds read.
 __global__ void embed_kernel(const int* __restrict__ tok, const int* __restrict__ pos, const bf16* __restrict__ E,
-                             const float* __restrict__ P, float* __restrict__ x, int d) {
+                             const float* __restrict__ P, float* __restrict__ x, int d, int n_vocab, int n_pos) {
   const int r = blockIdx.x;
-  const long long t = tok[r], p = pos[r];
+  const long long t = min(max(tok[r], 0), n_vocab - 1), p = min(max(pos[r], 0), n_pos - 1);
   for (int c = threadIdx.x; c < d; c += blockDim.x) x[(long long)r * d + c] = bf2f(E[t * d + c]) + P[p * d + c];
 }
 
-void launch_embed(const int* tok, const int* pos, const bf16* E, const float* P, float* x, int rows, int d, hipStream_t st) {
+void launch_embed(const int* tok, const int* pos, const bf16* E, const float* P, float* x, int rows, int d, int n_vocab,
+                  int n_pos, hipStream_t st) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(256), 0, st, tok, pos, E, P, x, d);
+  hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(256), 0, st, tok, pos, E, P, x, d, n_vocab, n_pos);
   WM_LAUNCH_CHECK("embed_kernel");
 }
 
