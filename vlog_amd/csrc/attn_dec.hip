@@ -196,14 +196,29 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
   if (done && done[row_hyp[row]]) return;
   const int e = threadIdx.x;
   const long long pb = (long long)pair * splits;
-  float M = -INFINITY;
-  for (int s = 0; s < splits; ++s) M = fmaxf(M, part_m[pb + s]);
-  float L = 0.f, o = 0.f;
-  for (int s = 0; s < splits; ++s) {
-    const float w = exp2f(part_m[pb + s] - M);
-    L += part_l[pb + s] * w;
-    o += part_o[(pb + s) * HD + e] * w;
+  // every partial requested before any is used (a runtime loop over the splits paid one dependent round trip
+  // per split and operand: ~6 us per launch at 12 splits); sums in split order as before
+  constexpr int SMAX = 16;
+  float pm[SMAX], pl[SMAX], po[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) {
+    const long long q = pb + (s < splits ? s : 0);
+    pm[s] = part_m[q];
+    pl[s] = part_l[q];
+    po[s] = part_o[q * HD + e];
   }
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s)
+    if (s < splits) M = fmaxf(M, pm[s]);
+  float L = 0.f, o = 0.f;
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s)
+    if (s < splits) {
+      const float w = exp2f(pm[s] - M);
+      L += pl[s] * w;
+      o += po[s] * w;
+    }
   out[(long long)row * ldo + h * HD + e] = f2bf(o / L);
 }
 
@@ -240,6 +255,21 @@ __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int spl
   if (a.stat && tid == 0)
     atomicAdd(a.stat + ((bx + split) & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + RG * 2 * HD * 2));
 
+  // the first 128-key chunk's K and V rows are requested before the q load (they do not depend on it): one
+  // memory round trip for both instead of two in sequence
+  bf16x8 kr[4], vr[4];
+  bool ok[4];
+  auto load_chunk = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = kb + u * 32 + wv * 8 + g;
+      ok[u] = p < nk;
+      const int pc = ok[u] ? p : 0;
+      kr[u] = ld_stream(K + (long long)pc * HD);
+      vr[u] = ld_stream(V + (long long)pc * HD);
+    }
+  };
+  load_chunk(0);
   float qf[RG][8];
   if (a.q_part) {
     // the cq split-K slabs summed into q by the whole block in ONE memory round trip (every slab load of a
@@ -282,16 +312,7 @@ __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int spl
     for (int i = 0; i < 8; ++i) o[r][i] = 0.f;
   }
   for (int kb = 0; kb < nk; kb += 128) {
-    bf16x8 kr[4], vr[4];
-    bool ok[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int p = kb + u * 32 + wv * 8 + g;
-      ok[u] = p < nk;
-      const int pc = ok[u] ? p : 0;
-      kr[u] = ld_stream(K + (long long)pc * HD);
-      vr[u] = ld_stream(V + (long long)pc * HD);
-    }
+    if (kb > 0) load_chunk(kb);
 #pragma unroll
     for (int r = 0; r < RG; ++r) {
       float sc[4];
@@ -444,21 +465,27 @@ static void launch_group(int n_items, int cap, const DecAttnArgs& a, hipStream_t
 // lane groups get theirs by shuffle; every lane then issues the K and V rows of all its keys of the chunk (16 or 32
 // x 16 B in flight) before using them.  Online softmax
 // per lane group, merged by xor-shuffles; lanes 0-7 store the 64 outputs (16 B each).
+// KSPLIT (few pairs: one window's beam): one BLOCK per (row, head), its 4 waves take contiguous quarters of the
+// keys and merge (m, l, o) through LDS in wave order, so a long history costs one chunk per wave instead of a
+// chain of dependent chunks in one wave.
+template <bool KSPLIT>
 __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int n_pairs) {
-  const int lane = threadIdx.x & 63;
-  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (pair >= n_pairs) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int pair = KSPLIT ? (int)blockIdx.x : (int)blockIdx.x * 4 + wv;
+  if (pair >= n_pairs) return;                         // KSPLIT: uniform over the block
   const int sub = lane & 7, g = lane >> 3;
   const int H = a.H;
   const int row = pair / H, h = pair - row * H;
   const int hyp = a.row_hyp[row];
   if (a.done && a.done[hyp]) return;
   const int nk = a.row_pos[row] + 1;
+  const int kbeg = KSPLIT ? wv * nk / 4 : 0, kend = KSPLIT ? (wv + 1) * nk / 4 : nk;
   const int* lrow = a.lin ? a.lin + (long long)hyp * a.n_ctx : nullptr;
   const long long hstride = (long long)H * a.n_ctx * HD;
   const bf16* K = a.kbase + (long long)h * a.n_ctx * HD + sub * 8;
   const bf16* V = a.vbase + (long long)h * a.n_ctx * HD + sub * 8;
-  if (a.stat && lane == 0) atomicAdd(a.stat + (pair & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
+  if (a.stat && lane == 0 && (!KSPLIT || wv == 0))
+    atomicAdd(a.stat + (pair & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
   float qf[8];
   load8(a.q + (long long)row * a.ldq + h * HD + sub * 8, qf);
 #pragma unroll
@@ -474,14 +501,14 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int pl = kb + 64 * j + lane;
-      phl[j] = (lrow && pl < nk) ? lrow[pl] : hyp;
+      phl[j] = (lrow && pl < kend) ? lrow[pl] : hyp;
     }
     bf16x8 kr[U], vr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int p = kb + u * 8 + g;
       const int ph = __shfl(phl[u >> 3], (u & 7) * 8 + g, 64);
-      const int pc = p < nk ? p : 0;
+      const int pc = p < kend ? p : 0;
       const long long ro = (long long)ph * hstride + (long long)pc * HD;
       kr[u] = *(const bf16x8*)(K + ro);
       vr[u] = *(const bf16x8*)(V + ro);
@@ -495,7 +522,7 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
       d += __shfl_xor(d, 4, 64);
-      sc[u] = (kb + u * 8 + g) < nk ? d : -INFINITY;
+      sc[u] = (kb + u * 8 + g) < kend ? d : -INFINITY;
     }
     float mx = m;
 #pragma unroll
@@ -519,8 +546,8 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
     m = mx;
   };
   // 128-key chunks while more than 64 keys remain (one memory round trip per 128 keys), a 64-key chunk for the rest
-  for (int kb = 0; kb < nk;) {
-    if (nk - kb > 64) {
+  for (int kb = kbeg; kb < kend;) {
+    if (kend - kb > 64) {
       chunk(std::integral_constant<int, 16>{}, kb);
       kb += 128;
     } else {
@@ -543,7 +570,35 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
     }
     m = M;
   }
-  if (g == 0) {
+  if constexpr (KSPLIT) {
+    // the 4 waves' (m, l, o) merged in wave order (a wave with no keys has m = -inf, l = 0, o = 0)
+    __shared__ float s_o[4][HD], s_ml[4][2];
+    if (g == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s_o[wv][sub * 8 + i] = o[i];
+      if (sub == 0) { s_ml[wv][0] = m; s_ml[wv][1] = l; }
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_ml[w][0]);
+    float L = 0.f, O[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float c = exp2f(s_ml[w][0] - M);
+      L += s_ml[w][1] * c;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) O[i] += s_o[w][sub * 8 + i] * c;
+    }
+    if (g == 0) {
+      const float inv = 1.0f / L;
+      bf16x8 r;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = f2bf(O[i] * inv);
+      *(bf16x8*)(a.out + (long long)row * a.ldo + h * HD + sub * 8) = r;
+    }
+  } else if (g == 0) {
     const float inv = 1.0f / l;
     bf16x8 r;
 #pragma unroll
@@ -571,9 +626,17 @@ void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* 
   a.out = out; a.ldo = ldo; a.H = H; a.T = n_ctx; a.n_ctx = n_ctx; a.splits = 1;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;
   const int n_pairs = rows * H;
-  const dim3 grid((n_pairs + 3) / 4);
-  if (ev0) hipExtLaunchKernelGGL(self_attn_wave_kernel, grid, dim3(256), 0, st, ev0, ev1, 0, a, n_pairs);
-  else hipLaunchKernelGGL(self_attn_wave_kernel, grid, dim3(256), 0, st, a, n_pairs);
+  // few (row, head) pairs (one window's beam, a few windows): a block per pair, keys split over its 4 waves.  A
+  // function of the pass's rows, so a row's arithmetic does not depend on how a pass is sliced
+  const bool ksplit = n_pairs <= 256;
+  const dim3 grid(ksplit ? n_pairs : (n_pairs + 3) / 4);
+  if (ksplit) {
+    if (ev0) hipExtLaunchKernelGGL(self_attn_wave_kernel<true>, grid, dim3(256), 0, st, ev0, ev1, 0, a, n_pairs);
+    else hipLaunchKernelGGL(self_attn_wave_kernel<true>, grid, dim3(256), 0, st, a, n_pairs);
+  } else {
+    if (ev0) hipExtLaunchKernelGGL(self_attn_wave_kernel<false>, grid, dim3(256), 0, st, ev0, ev1, 0, a, n_pairs);
+    else hipLaunchKernelGGL(self_attn_wave_kernel<false>, grid, dim3(256), 0, st, a, n_pairs);
+  }
   WM_LAUNCH_CHECK("self_attn_wave_kernel");
 }
 
