@@ -276,19 +276,30 @@ __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int spl
     // value issued before any add), in slab order plus the bias as splitk_reduce_kernel does (bit-identical
     // to the unfused bf16 q); the rows go through LDS.  (Per lane and row, a runtime loop over the slabs paid
     // one dependent round trip per slab and row: ~18 us per launch at 5 rows x 4 slabs.)
+    // (a thread's NIT values are unrolled too: their loads go out together, not one round trip per value)
     const long long slab = (long long)a.q_rows * a.ldq;
-    for (int idx = tid; idx < RG * HD; idx += 256) {
+    constexpr int NIT = (RG * HD + 255) / 256;
+    float pv[NIT][QMAXS], bq[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = min(tid + 256 * it, RG * HD - 1);
       const int r = idx / HD, e = idx - r * HD;
       const float* pq = a.q_part + (long long)(row0 + r) * a.ldq + h * HD + e;
-      float pv[QMAXS];
 #pragma unroll
       for (int sp = 0; sp < QMAXS; ++sp)
-        if (sp < a.q_splits) pv[sp] = pq[sp * slab];
+        if (sp < a.q_splits) pv[it][sp] = pq[sp * slab];
+      bq[it] = a.q_bias[h * HD + e];
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx >= RG * HD) break;
+      const int r = idx / HD, e = idx - r * HD;
       float v = 0.f;
 #pragma unroll
       for (int sp = 0; sp < QMAXS; ++sp)
-        if (sp < a.q_splits) v += pv[sp];
-      s_q[r][e] = bf2f(f2bf(v + a.q_bias[h * HD + e]));
+        if (sp < a.q_splits) v += pv[it][sp];
+      s_q[r][e] = bf2f(f2bf(v + bq[it]));
     }
     __syncthreads();
 #pragma unroll

@@ -780,7 +780,7 @@ void reserve(wm_engine* e, int n_slots, int n_hyp) {
     e->d_n_fin.ensure(nh * 4);
   }
   e->d_n_active.ensure(4);
-  e->d_suppress.ensure((size_t)m.n_vocab);
+  e->d_suppress.ensure((size_t)SEARCH_SB * 8);
   e->d_head_map.ensure((size_t)H * 4);
 }
 
@@ -827,7 +827,9 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   HIP_OK(hipMemcpyAsync(e->d_n_fin.p, zeros.data(), NH * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_cum.p, cum.data(), NH * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_hyp_slot.p, hyp_slot.data(), NH * 4, hipMemcpyHostToDevice, st));
-  HIP_OK(hipMemcpyAsync(e->d_suppress.p, sup.data(), V, hipMemcpyHostToDevice, st));
+  std::vector<unsigned long long> supbits(SEARCH_SB);
+  search_suppress_bits(sup.data(), V, supbits.data());
+  HIP_OK(hipMemcpyAsync(e->d_suppress.p, supbits.data(), SEARCH_SB * 8, hipMemcpyHostToDevice, st));
   int n_active = NH;
   HIP_OK(hipMemcpyAsync(e->d_n_active.p, &n_active, 4, hipMemcpyHostToDevice, st));
 
@@ -869,7 +871,14 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   std::memset(&sp, 0, sizeof(sp));
   sp.logits = logits; sp.ldl = V; sp.V = V;
   sp.tokens = e->d_tokens.as<int>(); sp.n_ctx = C; sp.seq_len = e->d_seq_len.as<int>(); sp.sample_begin = P;
-  sp.suppress = e->d_suppress.as<unsigned char>(); sp.suppress_blank = a->suppress_blank; sp.blank = m.blank;
+  sp.suppress_bits = e->d_suppress.as<unsigned long long>();
+  {
+    static const int sel_abl = [] {
+      const char* v = std::getenv("VLOG_AMD_SEL_ABL");
+      return v ? std::atoi(v) : 0;
+    }();
+    sp.abl = sel_abl;
+  } sp.suppress_blank = a->suppress_blank; sp.blank = m.blank;
   sp.eot = m.eot; sp.no_timestamps = m.no_timestamps; sp.ts_begin = m.timestamp_begin;
   sp.max_initial = a->max_initial_timestamp_index; sp.with_ts = a->with_timestamps; sp.done = e->d_done.as<int>();
   sp.mode = beam ? 1 : (sampling ? 2 : 0); sp.topk = beam ? a->beam_size + 1 : 1;

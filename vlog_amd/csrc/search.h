@@ -1,6 +1,9 @@
 #pragma once
 #include "common.h"
 
+#define SEARCH_SB 1024           // threads per logits row (logits_select_kernel)
+#define SEARCH_PER 52            // ids per thread: vocab <= SEARCH_SB * SEARCH_PER = 53248
+
 struct SearchParams {
   const float* logits;   // [rows][V] f32, row r belongs to hypothesis r
   long long ldl;
@@ -9,7 +12,9 @@ struct SearchParams {
   int n_ctx;
   int* seq_len;          // [n_hyp]
   int sample_begin;      // prompt length
-  const unsigned char* suppress;   // [V] 1 = suppressed
+  // suppressed ids as per-thread bit words: bit k of word t <=> id t + k * SEARCH_SB is suppressed (or >= V); one
+  // 8-B load per thread instead of one dependent byte load per element (search_suppress_bits builds it)
+  const unsigned long long* suppress_bits;   // [SEARCH_SB]
   int suppress_blank, blank, eot, no_timestamps, ts_begin, max_initial;   // max_initial < 0: none
   int with_ts;
   int* done;             // [n_hyp]
@@ -19,6 +24,7 @@ struct SearchParams {
   unsigned long long seed;
   int step;
   int max_length;
+  int abl;               // diagnostics (VLOG_AMD_SEL_ABL): bit 1 = beam top-k by K rounds over the row
   // greedy / sampling state (updated in place)
   float* cum;            // [n_hyp]
   int* row_tok; int* row_pos;      // next step's decoder input per hypothesis
@@ -38,5 +44,7 @@ struct BeamParams {
 };
 
 void launch_logits_select(const SearchParams& p, int n_hyp, hipStream_t st);
+// host: the suppress_bits words for a vocabulary of V ids (sup[i] != 0: suppressed)
+void search_suppress_bits(const unsigned char* sup, int V, unsigned long long* bits /* [SEARCH_SB] */);
 void launch_beam_select(const BeamParams& p, int n_win, hipStream_t st);
 void launch_no_speech(const float* logits, long long ldl, int V, int rows, int no_speech, float* out, hipStream_t st);

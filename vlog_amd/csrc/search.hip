@@ -14,7 +14,7 @@
 #include <stdexcept>
 #include <string>
 
-#define SB 1024
+#define SB SEARCH_SB
 #define NW (SB / 64)
 #define KMAX 9
 
@@ -101,8 +101,8 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   const float* lg = p.logits + (long long)h * p.ldl;
   const int V = p.V;
   const bool ts_on = p.with_ts != 0;
+  const unsigned long long sup = p.suppress_bits[tid];
   auto masked = [&](int i) -> bool {
-    if (p.suppress[i]) return true;
     if (first && p.suppress_blank && (i == p.blank || i == p.eot)) return true;
     if (!ts_on) return false;
     if (i == p.no_timestamps) return true;
@@ -120,22 +120,23 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   // masked entries recorded in a bitmask; both passes then run on registers.  (The earlier form looped
   // over the row twice with one dependent global load per iteration: ~90 us per launch of exposed latency.)
   // Beam (MODE 1) extracts its top-k in a third pass over the same registers, once `forced` is known.
-  constexpr int PER = (53248 + SB - 1) / SB;               // vocab <= 53248
+  constexpr int PER = SEARCH_PER;                          // vocab <= 53248
   constexpr bool RES = true;
   float xv[RES ? PER : 1];
   unsigned long long live = 0;
   auto xat = [&](int k) -> float { return RES ? xv[k] : lg[tid + k * SB]; };
   if (RES) {
+    // 32-bit byte offsets from the row base (global_load_dword v, v_off, s_base): one offset register per
+    // load in flight instead of a 64-bit address each (that form spilled and waited on its spills), no
+    // branches; ids >= V re-read the last id (never live: suppress_bits)
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = tid + k * SB;
-      xv[RES ? k : 0] = i < V ? lg[i] : -INFINITY;
-    }
+    for (int k = 0; k < PER; ++k)
+      xv[RES ? k : 0] = *(const float*)((const char*)lg + (unsigned)(min(tid + k * SB, V - 1) * 4));
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int i = tid + k * SB;
-    if (i < V && !masked(i)) live |= 1ull << k;
+    if (!((sup >> k) & 1) && !masked(i)) live |= 1ull << k;
   }
   // pass 1: per-segment max / argmax (and Gumbel keys for sampling, local top-k for beam)
   Cand mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
@@ -187,15 +188,114 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   else Z = fmaxf(lse_t, lse_s) + log1pf(expf(-fabsf(lse_t - lse_s)));
 
   if (MODE == 1) {
-    // pass 3: the wave's top-K of the allowed set (timestamps only when forced), K rounds of a wave-wide
-    // (max, argmax) over the register-resident row with the winners cleared from an availability mask (no
-    // per-thread candidate list: with one beside the row the kernel spilled, ~155 us per launch); then
-    // thread 0 merges the per-wave winners (cursors in LDS, not in scratch)
+    // pass 3: the top-K of the allowed set (timestamps only when forced), in `better` order.  A threshold
+    // first: tau = the K-th best of the per-thread maxima (K distinct elements are >= tau, so every top-K
+    // element is too); the few elements >= tau are appended to an LDS list and wave 0 ranks them.  (The
+    // earlier form ran K rounds of a wave argmax over the whole register-resident row: K x 52 compare-selects
+    // per thread, ~79 us per launch at beam 5, one CU per hypothesis.)  A list that overflows (ties) falls
+    // back to that form, so the result is the exact top-K either way.
     unsigned long long avail = live;
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (forced && tid + k * SB < tb) avail &= ~(1ull << k);
     const int wv = tid >> 6, lane = tid & 63;
+    constexpr int LCAP = 256;
+    __shared__ Cand s_list[LCAP];
+    __shared__ int s_n;
+    __shared__ Cand s_tau;
+    {
+      Cand lb{-INFINITY, 0x7fffffff};        // this thread's best allowed element
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + k * SB;
+        if (((avail >> k) & 1) && better(xat(k), i, lb.v, lb.i)) { lb.v = xat(k); lb.i = i; }
+      }
+      for (int r = 0; r < K; ++r) {          // the wave's K best per-thread maxima
+        Cand best = lb;
+        int owner = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float v2 = __shfl_xor(best.v, o, 64);
+          const int i2 = __shfl_xor(best.i, o, 64);
+          const int ow2 = __shfl_xor(owner, o, 64);
+          if (better(v2, i2, best.v, best.i) || (v2 == best.v && i2 == best.i && ow2 < owner)) {
+            best.v = v2; best.i = i2; owner = ow2;
+          }
+        }
+        if (lane == 0) s_top[wv * KMAX + r] = best;
+        if (lane == owner) lb = Cand{-INFINITY, 0x7fffffff};
+      }
+    }
+    __shared__ int s_ptr[NW];
+    if (tid < NW) s_ptr[tid] = 0;
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    if (tid == 0) {                          // tau: the K-th of the merged per-wave lists
+      Cand tau{-INFINITY, 0x7fffffff};
+      for (int r = 0; r < K; ++r) {
+        Cand best{-INFINITY, 0x7fffffff};
+        int bw = -1;
+        for (int w = 0; w < NW; ++w) {
+          const int pp = s_ptr[w];
+          if (pp >= K) continue;
+          const Cand c = s_top[w * KMAX + pp];
+          if (better(c.v, c.i, best.v, best.i)) { best = c; bw = w; }
+        }
+        if (bw < 0) { tau = Cand{-INFINITY, 0x7fffffff}; break; }
+        ++s_ptr[bw];
+        tau = best;
+      }
+      s_tau = tau;
+    }
+    __syncthreads();
+    const Cand tau = s_tau;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * SB;
+      if (((avail >> k) & 1) && (better(xat(k), i, tau.v, tau.i) || (xat(k) == tau.v && i == tau.i))) {
+        const int at = atomicAdd(&s_n, 1);
+        if (at < LCAP) s_list[at] = Cand{xat(k), i};
+      }
+    }
+    __syncthreads();
+    const int n_list = s_n;
+    if (n_list <= LCAP && !(p.abl & 2)) {
+      if (wv == 0) {
+        Cand c[LCAP / 64];
+#pragma unroll
+        for (int j = 0; j < LCAP / 64; ++j)
+          c[j] = lane + 64 * j < n_list ? s_list[lane + 64 * j] : Cand{-INFINITY, 0x7fffffff};
+        for (int r = 0; r < K; ++r) {
+          Cand best = c[0];
+          int bj = 0;
+#pragma unroll
+          for (int j = 1; j < LCAP / 64; ++j)
+            if (better(c[j].v, c[j].i, best.v, best.i)) { best = c[j]; bj = j; }
+          int owner = lane;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            const float v2 = __shfl_xor(best.v, o, 64);
+            const int i2 = __shfl_xor(best.i, o, 64);
+            const int ow2 = __shfl_xor(owner, o, 64);
+            if (better(v2, i2, best.v, best.i) || (v2 == best.v && i2 == best.i && ow2 < owner)) {
+              best.v = v2; best.i = i2; owner = ow2;
+            }
+          }
+          if (lane == owner) {
+#pragma unroll
+            for (int j = 0; j < LCAP / 64; ++j)
+              if (j == bj) c[j] = Cand{-INFINITY, 0x7fffffff};
+          }
+          if (lane == 0) {
+            const bool none = best.v == -INFINITY;
+            p.cand_tok[(long long)h * p.topk + r] = none ? -1 : best.i;
+            p.cand_lp[(long long)h * p.topk + r] = none ? -INFINITY : best.v - Z;
+          }
+        }
+      }
+      return;
+    }
+    // overflow (many tied values): K rounds over the whole row
     for (int r = 0; r < K; ++r) {
       Cand best{-INFINITY, 0x7fffffff};
       int bk = -1;
@@ -217,7 +317,6 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
       if (lane == 0) s_top[wv * KMAX + r] = best;
       if (lane == owner && bk >= 0) avail &= ~(1ull << bk);
     }
-    __shared__ int s_ptr[NW];
     if (tid < NW) s_ptr[tid] = 0;
     __syncthreads();
     if (tid == 0) {
@@ -267,6 +366,17 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
       p.done[h] = 1;
       atomicSub(p.n_active, 1);
     }
+  }
+}
+
+void search_suppress_bits(const unsigned char* sup, int V, unsigned long long* bits) {
+  for (int t = 0; t < SB; ++t) {
+    unsigned long long w = 0;
+    for (int k = 0; k < 64; ++k) {
+      const long long i = t + (long long)k * SB;
+      if (i >= V || sup[i]) w |= 1ull << k;
+    }
+    bits[t] = w;
   }
 }
 
