@@ -93,14 +93,31 @@ def test_factored_generate_matches_projected(small_models, kw):
 
     (ra, sa), (rb, sb) = _both(eng, enc, W, 5 * W, run)
     same = sum(x.tokens == y.tokens for x, y in zip(ra, rb))
+    encf = enc.float().cpu().numpy()
     if kw:
-        assert same >= W - 1, f"{same}/{W} windows identical"
+        # beam search on random weights: the beams of near-tied hypotheses can part on bf16 noise between the two
+        # forms (tools/diag_xattn_beam.py: tiny, 2 of 4 windows parted, one of them onto a sequence the oracle scores
+        # HIGHER than its own beam result; teacher-forced logits of both forms are equally close to the oracle,
+        # tools/diag_xattn_rows.py).  So a window that differs must be EPS-optimal under the oracle's beam search in
+        # BOTH forms, every token rule-legal, as tests/test_gpu_decode.py requires of the default form.
+        from oracle.decode import generate_one, score_sequence
+        eps = {"tiny": 0.02, "base": 0.03, "small": 0.05}[dims.name]
+        opt = GenerateOptions(beam_size=5, suppress_tokens=_sup(st), max_length=100)
+        for w, (x, y) in enumerate(zip(ra, rb)):
+            if x.tokens != y.tokens:
+                cross = orc.cross_kv(encf[w: w + 1])
+                r = generate_one(orc, cross, prompt, st, opt)
+                for z in (x, y):
+                    ended = len(prompt) + len(z.tokens) < 100
+                    chosen, _, score = score_sequence(orc, cross, prompt, z.tokens, st, opt, ended)
+                    assert np.all(np.isfinite(chosen)), (w, z.tokens)
+                    assert score >= r.score - eps, (w, score, r.score)
+        assert same >= W // 2, f"{same}/{W} windows identical"
     else:
         # greedy on random weights: a window may flip at a near-tied step (bf16 noise between the two forms);
         # then BOTH forms must be epsilon-consistent under the oracle, tie-aware (tests/parity_util.py)
         eps = {"tiny": 0.02, "base": 0.03, "small": 0.05}[dims.name]
         opt = GenerateOptions(beam_size=1, suppress_tokens=_sup(st), max_length=100)
-        encf = enc.float().cpu().numpy()
         orc16 = OracleWhisper(orc.w, dims, np.float32, bf16_acts=True)     # the engine's numeric format
         for w, (x, y) in enumerate(zip(ra, rb)):
             if x.tokens != y.tokens:

@@ -102,20 +102,30 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   const int V = p.V;
   const bool ts_on = p.with_ts != 0;
   const unsigned long long sup = p.suppress_bits[tid];
-  auto masked = [&](int i) -> bool {
-    if (first && p.suppress_blank && (i == p.blank || i == p.eot)) return true;
-    if (!ts_on) return false;
-    if (i == p.no_timestamps) return true;
-    if (i >= tb) {
-      if (pair_rule == 1) return true;
-      if (i < bound) return true;
-      if (first && p.max_initial >= 0 && i > tb + p.max_initial) return true;
-    } else {
-      if (pair_rule == 2 && i < p.eot) return true;
-      if (first) return true;
-    }
-    return false;
+  // The rules as 64-bit masks over this thread's ids i = tid + k SB (bit k): every rule is a range or a single
+  // id, so each costs O(1) instead of a branch chain per element (the per-element form was most of the
+  // kernel's 11-17 k instructions of straight-line code)
+  auto ge_mask = [&](long long x) -> unsigned long long {   // ids >= x
+    const long long d = x - tid;
+    if (d <= 0) return ~0ull;
+    const long long k0 = (d + SB - 1) / SB;
+    return k0 >= 64 ? 0ull : (~0ull << k0);
   };
+  auto id_bit = [&](long long x) -> unsigned long long {    // the single id x
+    const long long d = x - tid;
+    return (d >= 0 && d % SB == 0 && d / SB < 64) ? (1ull << (d / SB)) : 0ull;
+  };
+  const unsigned long long ts_mask = ge_mask(tb);
+  unsigned long long rule = 0;
+  if (first && p.suppress_blank) rule |= id_bit(p.blank) | id_bit(p.eot);
+  if (ts_on) {
+    rule |= id_bit(p.no_timestamps);
+    if (pair_rule == 1) rule |= ts_mask;
+    rule |= ts_mask & ~ge_mask(bound);                                     // timestamps below the bound
+    if (first && p.max_initial >= 0) rule |= ts_mask & ge_mask((long long)tb + p.max_initial + 1);
+    if (pair_rule == 2) rule |= ~ts_mask & ~ge_mask(p.eot);                 // text below <|endoftext|>
+    if (first) rule |= ~ts_mask;
+  }
   // The row is loaded ONCE into registers (PER values per thread, every load issued before any is used),
   // masked entries recorded in a bitmask; both passes then run on registers.  (The earlier form looped
   // over the row twice with one dependent global load per iteration: ~90 us per launch of exposed latency.)
@@ -133,22 +143,19 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
     for (int k = 0; k < PER; ++k)
       xv[RES ? k : 0] = *(const float*)((const char*)lg + (unsigned)(min(tid + k * SB, V - 1) * 4));
   }
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int i = tid + k * SB;
-    if (!((sup >> k) & 1) && !masked(i)) live |= 1ull << k;
-  }
+  live = ~(sup | rule) & ((1ull << PER) - 1);
   // pass 1: per-segment max / argmax (and Gumbel keys for sampling, local top-k for beam)
   Cand mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
   Cand gt{-INFINITY, 0x7fffffff}, gs{-INFINITY, 0x7fffffff};
   const int K = MODE == 1 ? p.topk : 0;
-  // (explicit branches, not a reference chosen per element: a `Cand& m = is_ts ? ms : mt` put both in scratch)
+  // (explicit branches, not a reference chosen per element: a `Cand& m = is_ts ? ms : mt` put both in scratch;
+  // a select-only form of this pass spilled)
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (!((live >> k) & 1)) continue;
     const int i = tid + k * SB;
     const float x = xat(k);
-    const bool is_ts = i >= tb;
+    const bool is_ts = (ts_mask >> k) & 1;
     if (is_ts) {
       if (better(x, i, ms.v, ms.i)) { ms.v = x; ms.i = i; }
     } else {
@@ -172,8 +179,7 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (!((live >> k) & 1)) continue;
-    const int i = tid + k * SB;
-    if (i >= tb) ss += expf(xat(k) - ms.v);
+    if ((ts_mask >> k) & 1) ss += expf(xat(k) - ms.v);
     else st += expf(xat(k) - mt.v);
   }
   st = block_sum(st, sh_f);
@@ -195,9 +201,7 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
     // per thread, ~79 us per launch at beam 5, one CU per hypothesis.)  A list that overflows (ties) falls
     // back to that form, so the result is the exact top-K either way.
     unsigned long long avail = live;
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (forced && tid + k * SB < tb) avail &= ~(1ull << k);
+    if (forced) avail &= ts_mask;
     const int wv = tid >> 6, lane = tid & 63;
     constexpr int LCAP = 256;
     __shared__ Cand s_list[LCAP];
