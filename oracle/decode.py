@@ -154,7 +154,7 @@ def _beam(model, cross, prompt, st, opt: GenerateOptions) -> GenerateResult:
     return beam_many(model, cross, prompt, st, opt)[0]
 
 
-def beam_many(model, cross, prompt, st, opt: GenerateOptions) -> List[GenerateResult]:
+def beam_many(model, cross, prompt, st, opt: GenerateOptions, on_step=None) -> List[GenerateResult]:
     """Beam search over several windows in lockstep (`cross` = model.cross_kv(enc[W])): each window's beam
     bookkeeping is exactly the one-window search below; the decoder runs all W x K hypothesis rows at once
     (window-major, sharing their window's cross-attention K/V).  A finished window's rows keep decoding a dummy
@@ -180,6 +180,8 @@ def beam_many(model, cross, prompt, st, opt: GenerateOptions) -> List[GenerateRe
         src_all = np.arange(W * K)
         last = np.full(W * K, st.eot, dtype=np.int64)
         pos += 1
+        if on_step is not None:
+            on_step(pos, sum(done))
         for w in range(W):
             if done[w]:
                 continue

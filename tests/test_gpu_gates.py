@@ -139,7 +139,8 @@ def test_config5_beam5_identical_to_oracle_beam(lv3):
     ws = sample_indices(W, 8)
     from tests.parity_util import progress
     progress("beam5: oracle beam search over 8 windows")
-    refs = beam_many(lv3.orc, lv3.orc.cross_kv(lv3.enc_of(ws)), lv3.prompt, lv3.st, lv3.opt(beam=5))
+    refs = beam_many(lv3.orc, lv3.orc.cross_kv(lv3.enc_of(ws)), lv3.prompt, lv3.st, lv3.opt(beam=5),
+                     on_step=lambda pos, nd: pos % 16 == 0 and progress(f"beam5: oracle position {pos}, {nd}/8 windows done"))
     same = [r.tokens == list(res[w].tokens) for w, r in zip(ws, refs)]
     g = gate_windows(lv3.orc, lv3.enc_of, lv3.prompt, res, lv3.st, lv3.opt(beam=5), lv3.tok, windows=ws)
     g.pop("oracle_tokens")

@@ -9,6 +9,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
 TAG=${TAG:-r03}
+export VLOG_AMD_PROGRESS=$R/gpurun_out/progress_$TAG.log
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --durations=20 --timeout 600 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
   rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log
