@@ -140,7 +140,28 @@ typedef struct wm_generate_args {
   float* h_cum_logprob;          /* [n_windows] */
   float* h_no_speech;            /* [n_windows] */
   int32_t* h_steps;              /* [1] decoder steps run (incl. prefill) */
+  /* ---- ABI 2 (wm_abi_version() >= 2) */
+  /* Row-set decode (greedy, or sampling with num_hypotheses 1): at most max_rows windows decode at once (0: all);
+   * when one ends, its row takes the next window in h_slots order at the next host check (the new window's prompt
+   * is prefilled inside that step's decoder pass), so the step count follows the total work instead of the longest
+   * window.  Order the windows longest-expected first (vlog_amd/shard.py expected_tokens).  compact = 1: once no
+   * window is waiting, finished rows are dropped from the passes when the live rows fall to 5/8 of the pass (the
+   * step graph is re-captured for the new row count).  Each window's result is the same computation either way;
+   * the GEMM / attention routes follow the pass's row count, so results agree to f32 rounding, not bit for bit. */
+  int32_t max_rows;
+  int32_t compact;
+  /* Optional per-step records, [n_windows][max_length] (NULL: off): the log-prob (after the logit rules) of the
+   * token chosen at each generated step, the final <|endoftext|> included (h_lengths[w] + 1 entries when the window
+   * ended on it, else h_lengths[w]); and, greedy / sampling, the best log-prob among the other allowed tokens at that
+   * step.  Beam search records the chosen hypothesis' path. */
+  float* h_token_logprobs;
+  float* h_token_logprobs_other;
+  /* Optional statistics [4] (NULL: off): decoder passes, sum over decode passes of the rows in the pass, windows
+   * started after the first pass (refills), step graphs captured. */
+  int64_t* h_stats;
 } wm_generate_args;
+/* Failure contract: a NaN / inf logits row or a row whose rules allow no token, detected on the device, fails the
+ * call (-1, wm_last_error names the window and step) instead of emitting a token. */
 int wm_generate(wm_engine* e, const wm_generate_args* a, void* stream);
 
 /* Teacher-forced decoder forward over n_seq sequences of seq_len tokens (one window slot each): logits for
@@ -151,6 +172,13 @@ int wm_generate(wm_engine* e, const wm_generate_args* a, void* stream);
 int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_len, const int32_t* h_tokens,
                float* d_logits, int32_t last_only, const int32_t* h_align_heads, int32_t n_align, float* d_attn,
                void* stream);
+
+/* ctranslate2 Whisper.detect_language(encoder_output) [FW↑] (faster-whisper detect_language, reached from
+ * worker/transcription.py:105-111 with language=None): one decoder step from <|startoftranscript|> for each of n
+ * windows (slots h_slots), softmax over the n_langs language tokens starting at lang_begin, on the device.
+ * h_probs [n][n_langs], in language-token order. */
+int wm_detect_language(wm_engine* e, int32_t n, const int32_t* h_slots, int32_t lang_begin, int32_t n_langs,
+                       float* h_probs, void* stream);
 
 /* ctranslate2 Whisper.align(encoder_output, start_sequence, text_tokens, num_frames, median_filter_width)
  * [FW↑] for ONE window (faster-whisper find_alignment, word_timestamps=True): teacher-forced decoder pass over
@@ -230,8 +258,13 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   kernel's q load (the q' kernel's, in the factored form); bit 1 combines the key splits in-kernel (last-arriving split) instead of a combine
  *   launch.  Every setting of these three knobs gives bit-identical results.
  *   "encode_chunk" (default 160): windows per encoder pass inside wm_encode (~52 MB of activation scratch
- *   per large-v3 window). */
+ *   per large-v3 window).
+ *   "cross_fp8" (default 0): opt-in fp8 (OCP e4m3) cross memory in the factored form (changes numerics).
+ *   "debug_nan_row" (default -1, TEST ONLY): >= 0 overwrites logits row r of every decode pass of wm_generate with
+ *   NaN before token selection (exercises the failure contract of wm_generate). */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);
+/* The engine's current value of an option (every key wm_set_option accepts, incl. environment overrides). */
+int wm_get_option(wm_engine* e, const char* key, int64_t* value);
 /* As wm_profile(e, 1) but only the classes whose bit is set in class_mask are timed (0 disables), so a
  * timed run can keep events on the dominant kernel alone. */
 int wm_profile_select(wm_engine* e, uint32_t class_mask);

@@ -198,6 +198,70 @@ def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists
     return out
 
 
+def step_logprobs(x_row: np.ndarray, sampled: Sequence[int], tok: int, st, opt: GenerateOptions):
+    """The oracle's per-step record for the token `tok` chosen after `sampled`: (log-prob under the rules, log-prob
+    on the other side of the timestamp-forcing threshold, the forcing gap log P(timestamps) - max log P(text),
+    best log-prob among the other allowed tokens).  Restates search.hip's records (lp = logit - logsumexp of the
+    allowed set) on the oracle's logits row."""
+    xp = apply_rules(x_row, sampled, st, opt.suppress_tokens, opt.suppress_blank, opt.max_initial_timestamp_index,
+                     opt.with_timestamps, force_timestamps=False)
+    lpp = log_softmax(xp)
+    tb = st.timestamp_begin
+    gap, forced = 0.0, False
+    xo = xp
+    if opt.with_timestamps:
+        text_max = float(np.max(lpp[:tb]))
+        ts = float(np.logaddexp.reduce(lpp[tb:]))
+        if np.isfinite(text_max) and np.isfinite(ts):
+            gap = ts - text_max
+        forced = ts > text_max
+        xo = xp.copy()
+        xo[:tb] = -np.inf                       # the forced form
+    lpo = log_softmax(xo)
+    lp_on, lp_off = (lpo, lpp) if forced else (lpp, lpo)
+    other = lp_on.copy()
+    other[tok] = -np.inf
+    return float(lp_on[tok]), float(lp_off[tok]), gap, float(np.max(other))
+
+
+def oracle_records(orc, enc: np.ndarray, prompt: Sequence[int], seqs: Sequence[Sequence[int]], rep: int, st,
+                   opt: GenerateOptions):
+    """Teacher-force `seqs` (window-major groups of `rep` sequences per window of `enc`) through the oracle in ONE
+    decoder pass and return, per sequence, arrays (lp, lp_other_side_of_forcing, gap, best_other) over its steps
+    (the generated tokens plus the final <|endoftext|> when the sequence ended before max_length)."""
+    cross = orc.cross_kv(enc)
+    P = len(prompt)
+    L = max(1, max(len(s) for s in seqs))
+    toks = np.full((len(seqs), P + L), st.eot, dtype=np.int64)
+    for i, s in enumerate(seqs):
+        toks[i, :P] = prompt
+        toks[i, P:P + len(s)] = s
+    logits, _ = orc.decode(toks, cross)
+
+    def one(i):
+        s = seqs[i]
+        steps = list(s) + ([st.eot] if P + len(s) < opt.max_length else [])
+        return np.array([step_logprobs(logits[i, P - 1 + k], list(s[:k]), t, st, opt) for k, t in enumerate(steps)],
+                        dtype=np.float64).reshape(-1, 4)
+
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=8) as pool:        # numpy's row ops release the GIL
+        return list(pool.map(one, range(len(seqs))))
+
+
+def record_deviation(gpu_lp: np.ndarray, rec: np.ndarray, eps_tie: float = 0.05):
+    """|GPU record - oracle record| per step; at a step whose forcing gap the oracle itself sits within eps_tie of
+    (the threshold decision is then ill-conditioned at bf16 noise), the other side of the threshold also counts.
+    -> (deviation per step, number of tie steps where the other side was closer)."""
+    g = np.asarray(gpu_lp, dtype=np.float64)
+    assert g.shape[0] == rec.shape[0], (g.shape, rec.shape)
+    dev = np.abs(g - rec[:, 0])
+    tie = (np.abs(rec[:, 2]) <= eps_tie) & (np.abs(g - rec[:, 1]) < dev)
+    dev = np.where(tie, np.abs(g - rec[:, 1]), dev)
+    assert not np.isnan(dev).any(), "NaN in a per-step record"
+    return dev, int(tie.sum())
+
+
 def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateOptions, tokenizer,
                  windows: Optional[Sequence[int]] = None, chunk: int = 8, time_offset=lambda w: 0.0,
                  known: Optional[dict] = None) -> dict:

@@ -11,14 +11,14 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VLOG_AMD_LIB") or os.path.join(_HERE, "libwhisper_mi355.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # Every entry point include/whisper_mi355.h declares (tests check the library exports all of them).
 SYMBOLS = (
     "wm_create", "wm_destroy", "wm_last_error", "wm_abi_version", "wm_set_weight", "wm_weights_complete", "wm_weight_count", "wm_weight_info",
     "wm_logmel", "wm_logmel_finalize", "wm_encode", "wm_reserve", "wm_cross_kv", "wm_generate", "wm_forward",
-    "wm_frame_energy", "wm_pcm_from_s16", "wm_vad_probs", "wm_cross_fp8_quantize", "wm_align", "wm_align_batch", "wm_dtw", "wm_device_bytes", "wm_profile_classes", "wm_profile_name", "wm_profile", "wm_profile_select",
-    "wm_profile_read", "wm_set_option", "wm_encoder_attention",
+    "wm_detect_language", "wm_frame_energy", "wm_pcm_from_s16", "wm_vad_probs", "wm_cross_fp8_quantize", "wm_align", "wm_align_batch", "wm_dtw", "wm_device_bytes", "wm_profile_classes", "wm_profile_name", "wm_profile", "wm_profile_select",
+    "wm_profile_read", "wm_set_option", "wm_get_option", "wm_encoder_attention",
 )
 
 
@@ -39,6 +39,9 @@ class GenerateArgsC(C.Structure):
         ("h_tokens", C.POINTER(C.c_int32)), ("h_lengths", C.POINTER(C.c_int32)), ("h_scores", C.POINTER(C.c_float)),
         ("h_cum_logprob", C.POINTER(C.c_float)), ("h_no_speech", C.POINTER(C.c_float)),
         ("h_steps", C.POINTER(C.c_int32)),
+        # ABI 2
+        ("max_rows", C.c_int32), ("compact", C.c_int32), ("h_token_logprobs", C.POINTER(C.c_float)),
+        ("h_token_logprobs_other", C.POINTER(C.c_float)), ("h_stats", C.POINTER(C.c_int64)),
     ]
 
 
@@ -71,6 +74,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "wm_generate": (C.c_int, [vp, C.POINTER(GenerateArgsC), vp]),
         "wm_forward": (C.c_int, [vp, i32, C.POINTER(i32), i32, C.POINTER(i32), vp, i32, C.POINTER(i32), i32, vp, vp]),
         "wm_frame_energy": (C.c_int, [vp, vp, i64, i32, vp, vp]),
+        "wm_detect_language": (C.c_int, [vp, i32, C.POINTER(i32), i32, i32, C.POINTER(C.c_float), vp]),
         "wm_vad_probs": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
         "wm_pcm_from_s16": (C.c_int, [vp, vp, i64, vp, vp]),
         "wm_cross_fp8_quantize": (C.c_int, [vp, vp, i64, vp, vp, vp]),
@@ -86,6 +90,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "wm_profile": (C.c_int, [vp, i32]),
         "wm_profile_select": (C.c_int, [vp, C.c_uint32]),
         "wm_set_option": (C.c_int, [vp, C.c_char_p, i64]),
+        "wm_get_option": (C.c_int, [vp, C.c_char_p, C.POINTER(i64)]),
         "wm_encoder_attention": (C.c_int, [vp, vp, vp, i32, i32, vp]),
         "wm_profile_read": (C.c_int, [vp, i32, C.POINTER(i64), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),

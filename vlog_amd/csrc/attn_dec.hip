@@ -630,16 +630,18 @@ static void launch_k(bool self, dim3 grid, const DecAttnArgs& a, hipStream_t st,
 
 void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* vc, const int* lin, const int* row_hyp,
                       const int* row_pos, const int* done, bf16* out, long long ldo, int rows, int H, int n_ctx,
-                      unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                      unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, int plan_rows) {
   if (rows <= 0) return;
+  if (plan_rows < rows) plan_rows = rows;
   DecAttnArgs a{};
   a.q = q; a.ldq = ldq; a.kbase = kc; a.vbase = vc; a.row_hyp = row_hyp; a.row_pos = row_pos; a.done = done; a.lin = lin;
   a.out = out; a.ldo = ldo; a.H = H; a.T = n_ctx; a.n_ctx = n_ctx; a.splits = 1;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;
   const int n_pairs = rows * H;
   // few (row, head) pairs (one window's beam, a few windows): a block per pair, keys split over its 4 waves.  A
-  // function of the pass's rows, so a row's arithmetic does not depend on how a pass is sliced
-  const bool ksplit = n_pairs <= 256;
+  // function of the whole PASS's rows (plan_rows), not this launch's slice, so a row's summation order — and so
+  // its result, bit for bit — does not depend on how the pass is sliced (decode_split)
+  const bool ksplit = plan_rows * H <= 256;
   const dim3 grid(ksplit ? n_pairs : (n_pairs + 3) / 4);
   if (ksplit) {
     if (ev0) hipExtLaunchKernelGGL(self_attn_wave_kernel<true>, grid, dim3(256), 0, st, ev0, ev1, 0, a, n_pairs);

@@ -40,6 +40,19 @@ __device__ __forceinline__ float ordered_to_float(unsigned int u) {
   return __uint_as_float(u);
 }
 
+// Device error word of a decode (engine.cpp d_err): [0] = code, [1], [2] = where.  The first failure wins (the
+// host reads the word at every poll of a decode and at its end, and raises).  Global atomics (vector memory).
+#define WM_ERR_NONFINITE 1     // a logits row held NaN / inf among its allowed tokens
+#define WM_ERR_NO_TOKEN 2      // the logit rules left no allowed token
+#define WM_ERR_TOKEN_RANGE 3   // a decoder input token id / position outside its table
+__device__ __forceinline__ void wm_report_error(int* err, int code, int a, int b) {
+  if (!err) return;
+  if (atomicCAS(err, 0, code) == 0) {
+    atomicExch(err + 1, a);
+    atomicExch(err + 2, b);
+  }
+}
+
 // Cross-attention fusions (attn_dec.hip launch_cross_attn): read q as bf16(sum of split-K slabs + bias) and/or
 // combine the key splits in-kernel (last arriver per item, counter words zero between launches).
 struct CrossFuse {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -32,12 +33,12 @@ void launch_ordered_to_float(const unsigned int*, float*, hipStream_t);
 void launch_frame_energy(const float*, long long, int, int, float*, hipStream_t);
 void launch_pcm_s16(const short*, long long, float*, hipStream_t);
 void launch_layernorm(const float*, long long, const int*, int, int, const float*, const float*, bf16*, long long, hipStream_t);
-void launch_embed(const int*, const int*, const bf16*, const float*, float*, int, int, int, int, hipStream_t);
+void launch_embed(const int*, const int*, const bf16*, const float*, float*, int, int, int, int, hipStream_t, int*);
 void launch_im2col_conv1(const float*, long long, const int*, const int*, int, int, int, bf16*, hipStream_t);
 void launch_zero_pad_rows(bf16*, int, long long, int, hipStream_t);
 void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
 void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const int*, const int*, const int*, const int*,
-                      bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
+                      bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t, int);
 void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
                        long long, int, int, int, float*, float*, float*, float*, const int*, int, int, int,
                        const CrossFuse&, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
@@ -76,6 +77,10 @@ thread_local std::string g_err;
     if (e__ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e__)); \
   } while (0)
 
+// Bumped whenever a device buffer moves: a captured step graph holds raw pointers, so a decode loop that
+// captured one re-captures it when this changed (e.g. a refill pass that grew a scratch buffer).
+std::atomic<long long> g_realloc{0};
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -86,6 +91,7 @@ struct DevBuf {
     bytes = 0;
     HIP_OK(hipMalloc(&p, b));
     bytes = b;
+    ++g_realloc;
   }
   void release() {
     if (p) (void)hipFree(p);
@@ -143,6 +149,15 @@ struct wm_engine {
   DevBuf d_tokens, d_lin, d_seq_len, d_done, d_cum, d_row_tok, d_row_pos, d_row_hyp, d_hyp_slot, d_n_active;
   DevBuf d_suppress, d_cand_tok, d_cand_lp, d_fin_tok, d_fin_len, d_fin_cum, d_n_fin, d_ns, d_logit_rows;
   DevBuf d_prow_tok, d_prow_pos, d_prow_hyp, d_head_map;
+  // d_n_active holds [0] the live-hypothesis counter and [1..3] the decode's device error word (common.h
+  // wm_report_error), so one poll copy reads both
+  // per-step records (wm_generate_args h_token_logprobs): per hypothesis, per finished beam candidate
+  DevBuf d_tok_lp, d_tok_lp_o, d_fin_lp;
+  // row-set decode (generate_rows): per-window prompts / slots, slot -> output id, output tables by window, and
+  // the event upload (pass rows, row set, logit rows, starts)
+  DevBuf d_win_prompt, d_win_slot, d_hyp_out, d_res_tok, d_res_len, d_res_cum, d_res_ns, d_res_lp, d_res_lp_o, d_ev;
+  std::vector<int> h_ev;     // host image of d_ev (kept alive until the next poll syncs the stream)
+  int dbg_nan_row = -1;      // TEST ONLY (wm_set_option "debug_nan_row"): NaN logits row before every selection
   // step activations
   DevBuf s_x, s_hb, s_q, s_ao, s_ff, s_logits, s_pm, s_pl, s_po;
   // profiler: per class, HIP event pairs recorded on the launch stream + algorithmic flops / bytes
@@ -562,7 +577,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   }
   {
     ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
-    launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b);
+    launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b,
+                     sl.total_rows);
   }
   gemm(DEC_OUT, amat(ao, d), W.out_w, d, d, d, ln_fuse ? resid_stat(W.out_b) : resid_ln(W.ln2_w, W.ln2_b, W.out_b));
   // cq: when the skinny split-K path runs it and no attention is captured, its slabs stay in the scratch and
@@ -656,7 +672,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
 void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos, const int* row_hyp, const int* done,
                   const int* lin, const int* logit_rows, int n_logit, float* logits,
                   const std::vector<std::vector<int>>* align_map, int n_align, float* attn, int cross_group,
-                  hipStream_t st) {
+                  hipStream_t st, int* err = nullptr) {
   const auto& m = e->dm;
   const int d = m.n_state, L = m.n_dec_layer;
   const auto& W0 = dec_weights(e)[0];
@@ -706,7 +722,7 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
     ProfScope ps(e, P_DEC_OTHER, s.st);
     float* x = e->s_x.as<float>() + (size_t)s.r0 * d;
     launch_embed(row_tok + s.r0, row_pos + s.r0, e->Wb("dec.embed"), e->Wf("dec.pos"), x, s.rows, d, m.n_vocab, m.n_text_ctx,
-                 s.st);
+                 s.st, err);
     launch_layernorm(x, d, nullptr, s.rows, d, W0.ln1_w, W0.ln1_b, e->s_hb.as<bf16>() + (size_t)s.r0 * d, d, s.st);
   }
   for (int l = 0; l < L; ++l) {
@@ -779,10 +795,102 @@ void reserve(wm_engine* e, int n_slots, int n_hyp) {
     e->d_fin_cum.ensure(nh * 16 * 4);
     e->d_n_fin.ensure(nh * 4);
   }
-  e->d_n_active.ensure(4);
+  e->d_n_active.ensure(8 * 4);
   e->d_suppress.ensure((size_t)SEARCH_SB * 8);
   e->d_head_map.ensure((size_t)H * 4);
 }
+
+// The decode's device error word (d_n_active[1..3]) -> exception (wm_generate returns -1 with this text).
+void check_decode_error(const int* w) {
+  if (w[0] == 0) return;
+  std::string what;
+  if (w[0] == WM_ERR_TOKEN_RANGE)
+    what = "decoder input token " + std::to_string(w[1]) + " at position " + std::to_string(w[2]) + " outside its table";
+  else
+    what = std::string(w[0] == WM_ERR_NONFINITE ? "non-finite (NaN / inf) logits" : "no token allowed by the logit rules") +
+           " for hypothesis " + std::to_string(w[1]) + " after " + std::to_string(w[2]) + " generated tokens";
+  throw std::runtime_error("generate: " + what + "; the decode was stopped");
+}
+
+// Search parameters shared by both decode loops (per-call fields: mode, tables, records)
+SearchParams search_params(wm_engine* e, const wm_generate_args* a, float* logits, int P) {
+  const auto& m = e->dm;
+  SearchParams sp;
+  std::memset(&sp, 0, sizeof(sp));
+  sp.logits = logits; sp.ldl = m.n_vocab; sp.V = m.n_vocab;
+  sp.tokens = e->d_tokens.as<int>(); sp.n_ctx = m.n_text_ctx; sp.seq_len = e->d_seq_len.as<int>(); sp.sample_begin = P;
+  sp.suppress_bits = e->d_suppress.as<unsigned long long>();
+  static const int sel_abl = [] {
+    const char* v = std::getenv("VLOG_AMD_SEL_ABL");
+    return v ? std::atoi(v) : 0;
+  }();
+  sp.abl = sel_abl;
+  sp.suppress_blank = a->suppress_blank; sp.blank = m.blank;
+  sp.eot = m.eot; sp.no_timestamps = m.no_timestamps; sp.ts_begin = m.timestamp_begin;
+  sp.max_initial = a->max_initial_timestamp_index; sp.with_ts = a->with_timestamps; sp.done = e->d_done.as<int>();
+  sp.seed = a->seed; sp.max_length = a->max_length;
+  sp.inv_temperature = a->temperature > 0.f ? 1.0f / a->temperature : 1.0f;
+  sp.cum = e->d_cum.as<float>(); sp.row_tok = e->d_row_tok.as<int>(); sp.row_pos = e->d_row_pos.as<int>();
+  sp.n_active = e->d_n_active.as<int>(); sp.cand_tok = e->d_cand_tok.as<int>(); sp.cand_lp = e->d_cand_lp.as<float>();
+  sp.err = e->d_n_active.as<int>() + 1;
+  return sp;
+}
+
+void upload_suppress(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
+  const int V = e->dm.n_vocab;
+  std::vector<unsigned char> sup(V, 0);
+  for (int i = 0; i < a->n_suppress; ++i)
+    if (a->h_suppress[i] >= 0 && a->h_suppress[i] < V) sup[a->h_suppress[i]] = 1;
+  std::vector<unsigned long long> supbits(SEARCH_SB);
+  search_suppress_bits(sup.data(), V, supbits.data());
+  HIP_OK(hipMemcpyAsync(e->d_suppress.p, supbits.data(), SEARCH_SB * 8, hipMemcpyHostToDevice, st));
+  HIP_OK(hipStreamSynchronize(st));
+}
+
+// TEST ONLY (option debug_nan_row): NaN into one logits row before selection (bytes 0xFF are a NaN)
+void debug_nan(wm_engine* e, float* logits, int rows, hipStream_t s) {
+  if (e->dbg_nan_row >= 0 && e->dbg_nan_row < rows)
+    HIP_OK(hipMemsetAsync(logits + (size_t)e->dbg_nan_row * e->dm.n_vocab, 0xFF, (size_t)e->dm.n_vocab * 4, s));
+}
+
+// One graph-replayed decode loop's capture state (see generate)
+struct StepGraph {
+  hipGraphExec_t exec = nullptr;
+  bool capturing = false;
+  long long gen = -1;                       // g_realloc at capture
+  void drop() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    exec = nullptr;
+  }
+  // false: buffers moved since the capture (the caller runs an eager step, which re-sizes, then captures again)
+  bool valid() const { return !exec || gen == g_realloc.load(); }
+  template <class F> void run(hipStream_t ds, F&& step) {
+    if (!exec) {
+      hipGraph_t g = nullptr;
+      gen = g_realloc.load();
+      HIP_OK(hipStreamBeginCapture(ds, hipStreamCaptureModeThreadLocal));
+      capturing = true;
+      step();
+      capturing = false;
+      HIP_OK(hipStreamEndCapture(ds, &g));
+      const hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIP_OK(ie);
+      if (gen != g_realloc.load()) throw std::runtime_error("decode step graph: a buffer moved during capture");
+    }
+    HIP_OK(hipGraphLaunch(exec, ds));
+  }
+  void abort(hipStream_t ds) {            // leave the stream out of capture mode before reporting an error
+    if (capturing) {
+      hipGraph_t g = nullptr;
+      if (hipStreamEndCapture(ds, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+      capturing = false;
+    }
+    drop();
+  }
+};
+
+void generate_rows(wm_engine* e, const wm_generate_args* a, hipStream_t st);
 
 void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   check_weights(e);
@@ -799,7 +907,16 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   if (beam && a->beam_size > 8) throw std::runtime_error("generate: beam_size <= 8 supported");
   for (int w = 0; w < W; ++w)
     if (a->h_slots[w] < 0 || a->h_slots[w] >= e->n_slots) throw std::runtime_error("generate: slot out of range");
+  for (int i = 0; i < W * P; ++i)
+    if (a->h_prompts[i] < 0 || a->h_prompts[i] >= V) throw std::runtime_error("generate: prompt token out of the vocabulary");
+  if (a->max_rows < 0) throw std::runtime_error("generate: max_rows must be >= 0");
+  if (per == 1 && !beam && ((a->max_rows > 0 && a->max_rows < W) || a->compact)) {
+    generate_rows(e, a, st);
+    return;
+  }
+  if (a->max_rows > 0 && a->max_rows < W) throw std::runtime_error("generate: max_rows needs greedy or num_hypotheses 1");
   reserve(e, e->n_slots, NH);
+  const bool rec = a->h_token_logprobs != nullptr;
   const int max_cand = beam ? std::max(1, (int)std::lround(a->beam_size * a->patience)) : 0;
   if (max_cand > 16) throw std::runtime_error("generate: beam_size * patience must be <= 16");
 
@@ -817,9 +934,6 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     for (int p = 0; p < C; ++p) lin[(size_t)h * C + p] = (beam && p < P) ? w * per : h;
     if (beam && (h % per) != 0) cum[h] = -INFINITY;
   }
-  std::vector<unsigned char> sup(V, 0);
-  for (int i = 0; i < a->n_suppress; ++i)
-    if (a->h_suppress[i] >= 0 && a->h_suppress[i] < V) sup[a->h_suppress[i]] = 1;
   HIP_OK(hipMemcpyAsync(e->d_tokens.p, tokens.data(), tokens.size() * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_lin.p, lin.data(), lin.size() * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_seq_len.p, seq_len.data(), NH * 4, hipMemcpyHostToDevice, st));
@@ -827,11 +941,14 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   HIP_OK(hipMemcpyAsync(e->d_n_fin.p, zeros.data(), NH * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_cum.p, cum.data(), NH * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_hyp_slot.p, hyp_slot.data(), NH * 4, hipMemcpyHostToDevice, st));
-  std::vector<unsigned long long> supbits(SEARCH_SB);
-  search_suppress_bits(sup.data(), V, supbits.data());
-  HIP_OK(hipMemcpyAsync(e->d_suppress.p, supbits.data(), SEARCH_SB * 8, hipMemcpyHostToDevice, st));
-  int n_active = NH;
-  HIP_OK(hipMemcpyAsync(e->d_n_active.p, &n_active, 4, hipMemcpyHostToDevice, st));
+  upload_suppress(e, a, st);
+  const int counter0[4] = {NH, 0, 0, 0};          // live hypotheses; error word cleared
+  HIP_OK(hipMemcpyAsync(e->d_n_active.p, counter0, sizeof(counter0), hipMemcpyHostToDevice, st));
+  if (rec) {
+    e->d_tok_lp.ensure((size_t)NH * C * 4);
+    if (!beam) e->d_tok_lp_o.ensure((size_t)NH * C * 4);
+    else e->d_fin_lp.ensure((size_t)W * max_cand * C * 4);
+  }
 
   // ---- prefill: rows (h, p) for every prompt position of every prefilled hypothesis (beam: one per window)
   const int pf_per = beam ? per : 1;                 // hypotheses per prefilled row set
@@ -863,28 +980,17 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     HIP_OK(hipStreamSynchronize(st));   // host vectors above go out of scope
   }
   float* logits = e->s_logits.as<float>();
+  int* err = e->d_n_active.as<int>() + 1;
   decoder_pass(e, rows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_prow_hyp.as<int>(), nullptr,
-               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, logits, nullptr, 0, nullptr, (per / pf_per) * P, st);
+               e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, logits, nullptr, 0, nullptr, (per / pf_per) * P, st, err);
   if (a->sot_index >= 0) launch_no_speech(logits + (size_t)NH * V, V, V, NH, m.no_speech, e->d_ns.as<float>(), st);
 
-  SearchParams sp;
-  std::memset(&sp, 0, sizeof(sp));
-  sp.logits = logits; sp.ldl = V; sp.V = V;
-  sp.tokens = e->d_tokens.as<int>(); sp.n_ctx = C; sp.seq_len = e->d_seq_len.as<int>(); sp.sample_begin = P;
-  sp.suppress_bits = e->d_suppress.as<unsigned long long>();
-  {
-    static const int sel_abl = [] {
-      const char* v = std::getenv("VLOG_AMD_SEL_ABL");
-      return v ? std::atoi(v) : 0;
-    }();
-    sp.abl = sel_abl;
-  } sp.suppress_blank = a->suppress_blank; sp.blank = m.blank;
-  sp.eot = m.eot; sp.no_timestamps = m.no_timestamps; sp.ts_begin = m.timestamp_begin;
-  sp.max_initial = a->max_initial_timestamp_index; sp.with_ts = a->with_timestamps; sp.done = e->d_done.as<int>();
+  SearchParams sp = search_params(e, a, logits, P);
   sp.mode = beam ? 1 : (sampling ? 2 : 0); sp.topk = beam ? a->beam_size + 1 : 1;
-  sp.inv_temperature = sampling ? 1.0f / a->temperature : 1.0f; sp.seed = a->seed; sp.max_length = a->max_length;
-  sp.cum = e->d_cum.as<float>(); sp.row_tok = e->d_row_tok.as<int>(); sp.row_pos = e->d_row_pos.as<int>();
-  sp.n_active = e->d_n_active.as<int>(); sp.cand_tok = e->d_cand_tok.as<int>(); sp.cand_lp = e->d_cand_lp.as<float>();
+  if (rec) {
+    sp.tok_lp = e->d_tok_lp.as<float>();
+    if (!beam) sp.tok_lp_other = e->d_tok_lp_o.as<float>();
+  }
   BeamParams bp;
   std::memset(&bp, 0, sizeof(bp));
   bp.beam = a->beam_size; bp.max_cand = max_cand; bp.n_ctx = C; bp.sample_begin = P; bp.max_length = a->max_length;
@@ -892,15 +998,22 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   bp.seq_len = sp.seq_len; bp.cum = sp.cum; bp.done = sp.done; bp.row_tok = sp.row_tok; bp.row_pos = sp.row_pos;
   bp.fin_tok = e->d_fin_tok.as<int>(); bp.fin_len = e->d_fin_len.as<int>(); bp.fin_cum = e->d_fin_cum.as<float>();
   bp.n_fin = e->d_n_fin.as<int>(); bp.n_active = sp.n_active;
+  if (rec && beam) {
+    bp.tok_lp = e->d_tok_lp.as<float>();
+    bp.fin_lp = e->d_fin_lp.as<float>();
+  }
 
   auto select = [&](int step) {
     sp.step = step;
+    debug_nan(e, logits, NH, st);
     ProfScope ps(e, P_SELECT, st);
     launch_logits_select(sp, NH, st);
     if (beam) launch_beam_select(bp, W, st);
   };
   select(0);
   int steps = 1;
+  long long row_steps = 0;
+  int captures = 0;
   const int max_steps = a->max_length - P;      // generated tokens (incl. the final one) <= max_length - P
   const int check = std::max(1, a->check_every);
   // A decode step's launches are identical from step to step: every per-step quantity (tokens, positions,
@@ -928,66 +1041,65 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     // greedy / sampling never reorder hypotheses: the lineage table is the identity and self-attention
     // reads each row's own cache directly (no dependent lineage load per key block)
     decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                 beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, s);
+                 beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, s, err);
     sp.step = step;
+    debug_nan(e, logits, NH, s);
     launch_logits_select(sp, NH, s);
     if (beam) launch_beam_select(bp, W, s);
   };
+  StepGraph graph;
+  int poll[4] = {0, 0, 0, 0};                   // live count + error word
   try {
     for (int step = 1; step < max_steps; ++step) {
       if ((step - 1) % check == 0) {
-        int act = 0;
-        HIP_OK(hipMemcpyAsync(&act, e->d_n_active.p, 4, hipMemcpyDeviceToHost, ds));
+        HIP_OK(hipMemcpyAsync(poll, e->d_n_active.p, sizeof(poll), hipMemcpyDeviceToHost, ds));
         HIP_OK(hipStreamSynchronize(ds));
-        if (act <= 0) break;
+        check_decode_error(poll + 1);
+        if (poll[0] <= 0) break;
       }
       if (!use_graph || step == 1) {
         if (use_graph) step_eager(step, ds);
         else {
           decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                       beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, st);
+                       beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, st, err);
           select(step);
         }
       } else {
-        if (!gexec) {
-          hipGraph_t g = nullptr;
-          HIP_OK(hipStreamBeginCapture(ds, hipStreamCaptureModeThreadLocal));
-          capturing = true;
-          step_eager(step, ds);
-          capturing = false;
-          HIP_OK(hipStreamEndCapture(ds, &g));
-          const hipError_t ie = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
-          (void)hipGraphDestroy(g);
-          HIP_OK(ie);
-        }
-        HIP_OK(hipGraphLaunch(gexec, ds));
+        if (!graph.exec) ++captures;
+        graph.run(ds, [&] { step_eager(step, ds); });
       }
       ++steps;
+      row_steps += NH;
     }
   } catch (...) {
-    if (capturing) {                           // leave the stream out of capture mode before reporting
-      hipGraph_t g = nullptr;
-      if (hipStreamEndCapture(ds, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
-    }
-    if (gexec) (void)hipGraphExecDestroy(gexec);
+    graph.abort(ds);
     throw;
   }
   if (use_graph) {
     HIP_OK(hipEventRecord(e->ev_g1, ds));
     HIP_OK(hipStreamWaitEvent(st, e->ev_g1, 0));
   }
-  if (gexec) {
+  if (graph.exec) {
     HIP_OK(hipStreamSynchronize(ds));          // the graph's last replay has completed before it is destroyed
-    HIP_OK(hipGraphExecDestroy(gexec));
+    graph.drop();
   }
 
   // ---- results
   std::vector<int> out_tok((size_t)NH * C), out_len(NH);
-  std::vector<float> out_cum(NH), ns(NH, 0.f);
+  std::vector<float> out_cum(NH), ns(NH, 0.f), out_lp, out_lpo, fin_lp;
   HIP_OK(hipMemcpyAsync(out_tok.data(), e->d_tokens.p, out_tok.size() * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(out_len.data(), e->d_seq_len.p, NH * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(out_cum.data(), e->d_cum.p, NH * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(poll, e->d_n_active.p, sizeof(poll), hipMemcpyDeviceToHost, st));
   if (a->sot_index >= 0) HIP_OK(hipMemcpyAsync(ns.data(), e->d_ns.p, NH * 4, hipMemcpyDeviceToHost, st));
+  if (rec) {
+    out_lp.resize((size_t)NH * C);
+    HIP_OK(hipMemcpyAsync(out_lp.data(), e->d_tok_lp.p, out_lp.size() * 4, hipMemcpyDeviceToHost, st));
+    if (!beam) {
+      out_lpo.resize((size_t)NH * C);
+      HIP_OK(hipMemcpyAsync(out_lpo.data(), e->d_tok_lp_o.p, out_lpo.size() * 4, hipMemcpyDeviceToHost, st));
+    }
+  }
   std::vector<int> fin_tok, fin_len, n_fin;
   std::vector<float> fin_cum;
   if (beam) {
@@ -997,20 +1109,28 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     HIP_OK(hipMemcpyAsync(fin_len.data(), e->d_fin_len.p, fin_len.size() * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(fin_cum.data(), e->d_fin_cum.p, fin_cum.size() * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(n_fin.data(), e->d_n_fin.p, W * 4, hipMemcpyDeviceToHost, st));
+    if (rec) {
+      fin_lp.resize((size_t)W * max_cand * C);
+      HIP_OK(hipMemcpyAsync(fin_lp.data(), e->d_fin_lp.p, fin_lp.size() * 4, hipMemcpyDeviceToHost, st));
+    }
   }
   HIP_OK(hipStreamSynchronize(st));
+  check_decode_error(poll + 1);
   const float lp = a->length_penalty;
   auto norm = [&](float c, int n) { return c / std::pow((float)std::max(n, 1), lp); };
+  const int ML = a->max_length;
   for (int w = 0; w < W; ++w) {
-    const int ML = a->max_length;
     int best_len = 0;
     float best_cum = 0.f, best_score = -INFINITY;
     const int* best_ptr = nullptr;
+    const float *best_lp = nullptr, *best_lpo = nullptr;   // records of the chosen hypothesis (first generated step)
     if (beam) {
-      struct C2 { const int* t; int n; float c; };
+      struct C2 { const int* t; int n; float c; const float* r; };
       std::vector<C2> cands;
-      for (int i = 0; i < n_fin[w]; ++i)
-        cands.push_back({&fin_tok[((size_t)w * max_cand + i) * C], fin_len[(size_t)w * max_cand + i], fin_cum[(size_t)w * max_cand + i]});
+      for (int i = 0; i < n_fin[w]; ++i) {
+        const size_t f = (size_t)w * max_cand + i;
+        cands.push_back({&fin_tok[f * C], fin_len[f], fin_cum[f], rec ? &fin_lp[f * C] : nullptr});
+      }
       if ((int)cands.size() < a->beam_size) {       // openai finalize: add unfinished beams by sum_logprob
         std::vector<int> order;
         for (int b = 0; b < per; ++b)
@@ -1019,19 +1139,22 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
         for (int b : order) {
           if ((int)cands.size() >= a->beam_size) break;
           const int h = w * per + b;
-          cands.push_back({&out_tok[(size_t)h * C + P], out_len[h] - P, out_cum[h]});
+          cands.push_back({&out_tok[(size_t)h * C + P], out_len[h] - P, out_cum[h], rec ? &out_lp[(size_t)h * C + P] : nullptr});
         }
       }
       for (const auto& c : cands) {
         const float s = norm(c.c, c.n);
-        if (s > best_score) { best_score = s; best_len = c.n; best_cum = c.c; best_ptr = c.t; }
+        if (s > best_score) { best_score = s; best_len = c.n; best_cum = c.c; best_ptr = c.t; best_lp = c.r; }
       }
     } else {
       for (int j = 0; j < per; ++j) {
         const int h = w * per + j;
         const int n = out_len[h] - P;
         const float s = norm(out_cum[h], n);
-        if (s > best_score) { best_score = s; best_len = n; best_cum = out_cum[h]; best_ptr = &out_tok[(size_t)h * C + P]; }
+        if (s > best_score) {
+          best_score = s; best_len = n; best_cum = out_cum[h]; best_ptr = &out_tok[(size_t)h * C + P];
+          if (rec) { best_lp = &out_lp[(size_t)h * C + P]; best_lpo = &out_lpo[(size_t)h * C + P]; }
+        }
       }
     }
     for (int i = 0; i < best_len && i < ML; ++i) a->h_tokens[(size_t)w * ML + i] = best_ptr[i];
@@ -1039,8 +1162,306 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     a->h_scores[w] = best_score;
     if (a->h_cum_logprob) a->h_cum_logprob[w] = best_cum;
     if (a->h_no_speech) a->h_no_speech[w] = ns[w * per];
+    if (rec) {
+      // one record per generated token, plus the final <|endoftext|> when the window ended on it
+      const int nr = std::min(ML, best_len + (P + best_len < ML ? 1 : 0));
+      for (int i = 0; i < nr; ++i) {
+        a->h_token_logprobs[(size_t)w * ML + i] = best_lp ? best_lp[i] : NAN;
+        if (a->h_token_logprobs_other) a->h_token_logprobs_other[(size_t)w * ML + i] = best_lpo ? best_lpo[i] : NAN;
+      }
+    }
+  }
+  if (a->h_stats) {
+    a->h_stats[0] = steps;
+    a->h_stats[1] = row_steps;
+    a->h_stats[2] = 0;
+    a->h_stats[3] = captures;
   }
   if (a->h_steps) a->h_steps[0] = steps;
+}
+
+// Row-set decode: greedy (or sampling with one hypothesis) over W windows with at most R = max_rows in flight.
+//
+// A batch of 30 s windows ends when its LONGEST window does (speech density varies: a few tokens for silence, 200+
+// for dense speech), and every decode step pays the weight-streaming GEMM chain however many rows are still live.
+// Here the decode keeps a ROW SET: hypothesis slot h of row r holds one window; when the host check finds rows
+// whose window ended, it starts the next windows (in h_slots order, which the host sorts longest-expected first)
+// in those rows.  The new windows' prompts are prefilled INSIDE that step's decoder pass (pass rows = one decode
+// row per live hypothesis + P prompt rows per new one; the final LayerNorm gathers one logits row per row-set row
+// in row order), so a refill costs no extra pass.  Rows stay in place while windows wait, so the captured step
+// graph stays valid; once the queue is empty and compaction is on, the live rows are packed densely when they
+// fall to 5/8 of the pass (re-capture for the new count).  A finished hypothesis' tokens are copied to the
+// per-window output tables by the block that ends it (search.hip), since its slot is then reused.
+void generate_rows(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
+  const auto& m = e->dm;
+  const int C = m.n_text_ctx, V = m.n_vocab;
+  const int W = a->n_windows, P = a->prompt_len;
+  const int R = a->max_rows > 0 ? std::min(a->max_rows, W) : W;
+  const bool rec = a->h_token_logprobs != nullptr;
+  const int ML = a->max_length;
+  reserve(e, e->n_slots, R);
+  // per-window inputs and outputs
+  e->d_win_prompt.ensure((size_t)W * P * 4);
+  e->d_win_slot.ensure((size_t)W * 4);
+  e->d_hyp_out.ensure((size_t)R * 4);
+  e->d_res_tok.ensure((size_t)W * C * 4);
+  e->d_res_len.ensure((size_t)W * 4);
+  e->d_res_cum.ensure((size_t)W * 4);
+  e->d_res_ns.ensure((size_t)W * 4);
+  if (rec) {
+    e->d_tok_lp.ensure((size_t)R * C * 4);
+    e->d_tok_lp_o.ensure((size_t)R * C * 4);
+    e->d_res_lp.ensure((size_t)W * C * 4);
+    e->d_res_lp_o.ensure((size_t)W * C * 4);
+  }
+  HIP_OK(hipMemcpyAsync(e->d_win_prompt.p, a->h_prompts, (size_t)W * P * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_win_slot.p, a->h_slots, (size_t)W * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemsetAsync(e->d_res_ns.p, 0, (size_t)W * 4, st));
+  HIP_OK(hipMemsetAsync(e->d_n_active.p, 0, 4 * 4, st));      // live counter, error word
+  {
+    std::vector<int> ones(R, 1);               // every slot starts ended (no hypothesis)
+    HIP_OK(hipMemcpyAsync(e->d_done.p, ones.data(), (size_t)R * 4, hipMemcpyHostToDevice, st));
+    upload_suppress(e, a, st);                 // (synchronises: `ones` goes out of scope)
+  }
+  // pass rows: R decode rows + P prompt rows per starting window; logits rows: R + one sot row per start
+  ensure_step(e, R * (1 + P), 2 * R);
+  float* logits = e->s_logits.as<float>();
+  int* counters = e->d_n_active.as<int>();     // [0] live hypotheses, [1..3] error word
+  int* err = counters + 1;
+  SearchParams sp = search_params(e, a, logits, P);
+  sp.mode = a->temperature > 0.f ? 2 : 0;
+  sp.topk = 1;
+  sp.row_hyp = e->d_row_hyp.as<int>();
+  sp.hyp_out = e->d_hyp_out.as<int>();
+  sp.res_tok = e->d_res_tok.as<int>(); sp.res_len = e->d_res_len.as<int>(); sp.res_cum = e->d_res_cum.as<float>();
+  if (rec) {
+    sp.tok_lp = e->d_tok_lp.as<float>(); sp.tok_lp_other = e->d_tok_lp_o.as<float>();
+    sp.res_lp = e->d_res_lp.as<float>(); sp.res_lp_other = e->d_res_lp_o.as<float>();
+  }
+
+  // host view: row r holds hypothesis slot row_hyp[r]; slot h decodes window hyp_win[h] while live[h]
+  std::vector<int> row_hyp(R), hyp_win(R, -1);
+  std::vector<char> live(R, 0);
+  for (int r = 0; r < R; ++r) row_hyp[r] = r;
+  int nrows = R, next = 0;
+  long long passes = 0, row_steps = 0, refills = 0;
+  int captures = 0;
+
+  // One event pass.  `carry` per new row: the old row index of a carried live row, -1 for a row whose slot starts
+  // a window (`starts`, in row order), -2 for an idle row (its slot ended; the selection skips it).
+  std::vector<int> carry, new_row_hyp;
+  std::vector<std::pair<int, int>> starts;      // (slot, window)
+  auto event = [&](hipStream_t s) {
+    const int nr = (int)new_row_hyp.size(), nst = (int)starts.size();
+    const int nsot = a->sot_index >= 0 ? nst : 0;
+    int np = 0, n_live = 0;
+    for (int c : carry) {
+      np += c >= 0 ? 1 : (c == -1 ? P : 0);
+      n_live += c >= -1;
+    }
+    // upload: ptok, ppos, phyp, psrc [np] | row set [nr] | logits rows [nr + nsot] | start slots, windows [nst] | live
+    std::vector<int>& u = e->h_ev;
+    u.assign((size_t)4 * np + 2 * nr + nsot + 2 * nst + 1, 0);
+    int* ptok = u.data(); int* ppos = ptok + np; int* phyp = ppos + np; int* psrc = phyp + np;
+    int* rh = psrc + np; int* lr = rh + nr; int* hs = lr + nr + nsot; int* ws = hs + nst;
+    ws[nst] = n_live;
+    int i = 0, k = 0;
+    for (int r = 0; r < nr; ++r) {
+      rh[r] = new_row_hyp[r];
+      if (carry[r] >= 0) {
+        phyp[i] = new_row_hyp[r]; psrc[i] = carry[r];
+        lr[r] = i++;
+      } else if (carry[r] == -1) {
+        const int h = starts[k].first, w = starts[k].second;
+        for (int p = 0; p < P; ++p, ++i) {
+          ptok[i] = a->h_prompts[(size_t)w * P + p]; ppos[i] = p; phyp[i] = h; psrc[i] = -1;
+          if (p == a->sot_index) lr[nr + k] = i;
+        }
+        lr[r] = i - 1;                          // the last prompt position predicts the first token
+        hs[k] = h; ws[k] = w;
+        ++k;
+      } else {
+        lr[r] = 0;
+      }
+    }
+    e->d_ev.ensure(u.size() * 4);
+    int* du = e->d_ev.as<int>();
+    HIP_OK(hipMemcpyAsync(du, u.data(), u.size() * 4, hipMemcpyHostToDevice, s));
+    int* dptok = du; int* dppos = du + np; int* dphyp = du + 2 * np; int* dpsrc = du + 3 * np;
+    int* drh = du + 4 * np; int* dlr = drh + nr; int* dhs = dlr + nr + nsot; int* dws = dhs + nst;
+    // carried rows read token / position from the last selection's (old) row order before it is overwritten
+    launch_rows_fill(np, dpsrc, dptok, dppos, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), s);
+    launch_hyp_start(nst, dhs, dws, e->d_win_prompt.as<int>(), P, e->d_win_slot.as<int>(), C, e->d_tokens.as<int>(),
+                     e->d_seq_len.as<int>(), e->d_done.as<int>(), e->d_cum.as<float>(), e->d_hyp_slot.as<int>(),
+                     e->d_hyp_out.as<int>(), s);
+    HIP_OK(hipMemcpyAsync(e->d_row_hyp.p, drh, (size_t)nr * 4, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipMemcpyAsync(counters, dws + nst, 4, hipMemcpyDeviceToDevice, s));
+    decoder_pass(e, np, dptok, dppos, dphyp, e->d_done.as<int>(), nullptr, dlr, nr + nsot, logits, nullptr, 0, nullptr, 1, s,
+                 err);
+    if (nsot) launch_no_speech(logits + (size_t)nr * V, V, V, nsot, m.no_speech, e->d_res_ns.as<float>(), s, dws);
+    debug_nan(e, logits, nr, s);
+    {
+      ProfScope ps(e, P_SELECT, s);
+      launch_logits_select(sp, nr, s);
+    }
+    // host view of the new row set
+    for (int r = 0; r < nr; ++r) row_hyp[r] = new_row_hyp[r];
+    for (const auto& sw : starts) { hyp_win[sw.first] = sw.second; live[sw.first] = 1; }
+    nrows = nr;
+    ++passes;
+    row_steps += nr;
+  };
+
+  const bool use_graph = e->dec_graph && !e->prof_on && !e->dec_split;
+  hipStream_t ds = st;
+  if (use_graph) {
+    if (!e->gst) {
+      HIP_OK(hipStreamCreateWithFlags(&e->gst, hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_g0, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_g1, hipEventDisableTiming));
+    }
+    HIP_OK(hipEventRecord(e->ev_g0, st));
+    HIP_OK(hipStreamWaitEvent(e->gst, e->ev_g0, 0));
+    ds = e->gst;
+  }
+  auto step_eager = [&](hipStream_t s) {
+    decoder_pass(e, nrows, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
+                 nullptr, nullptr, nrows, logits, nullptr, 0, nullptr, 1, s, err);
+    debug_nan(e, logits, nrows, s);
+    ProfScope ps(e, P_SELECT, s);
+    launch_logits_select(sp, nrows, s);
+  };
+
+  StepGraph graph;
+  bool graph_rows_changed = true;               // the next decode step runs eagerly (sizes scratch), then captures
+  const int check = std::max(1, a->check_every);
+  const int refill_min = std::max(1, R / 16);   // a refill pass runs eagerly: batch the starts
+  std::vector<int> h_done(R);
+  int h_cnt[4] = {0, 0, 0, 0};
+  // every window's tokens need at most max_length - P steps; a generous bound against a stuck loop
+  const long long pass_limit = (long long)(W / std::max(1, R) + 2) * (ML - P + check + 2) + 16;
+  try {
+    // first pass: the first R windows start
+    carry.assign(R, -1);
+    new_row_hyp.resize(R);
+    starts.clear();
+    for (int r = 0; r < R; ++r) {
+      new_row_hyp[r] = r;
+      starts.push_back({r, next++});
+    }
+    event(ds);
+    int k = 1;                                  // decode passes since the last host check
+    for (;;) {
+      if (k >= check) {
+        k = 0;
+        HIP_OK(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, ds));
+        HIP_OK(hipMemcpyAsync(h_done.data(), e->d_done.p, (size_t)R * 4, hipMemcpyDeviceToHost, ds));
+        HIP_OK(hipStreamSynchronize(ds));
+        check_decode_error(h_cnt + 1);
+        int n_live = 0, n_free = 0;
+        for (int r = 0; r < nrows; ++r) {
+          const int h = row_hyp[r];
+          if (live[h] && h_done[h]) live[h] = 0;
+          n_live += live[h];
+        }
+        n_free = nrows - n_live;
+        if (n_live == 0 && next >= W) break;
+        const bool refill = next < W && (n_free >= refill_min || n_live == 0);
+        const bool compact = next >= W && a->compact && n_live * 8 <= nrows * 5;
+        if (refill || compact) {
+          carry.clear(); new_row_hyp.clear(); starts.clear();
+          for (int r = 0; r < nrows; ++r) {
+            const int h = row_hyp[r];
+            if (live[h]) {
+              carry.push_back(r); new_row_hyp.push_back(h);
+            } else if (refill) {
+              if (next < W) {
+                carry.push_back(-1); new_row_hyp.push_back(h); starts.push_back({h, next++});
+                ++refills;
+              } else {
+                carry.push_back(-2); new_row_hyp.push_back(h);
+              }
+            }                                   // compact: ended rows leave the row set
+          }
+          const int before = nrows;
+          event(ds);
+          if (nrows != before) {
+            graph.drop();
+            graph_rows_changed = true;
+          }
+          k = 1;
+          continue;
+        }
+      }
+      if (!graph.valid()) {                     // an event pass grew a buffer the captured graph points into
+        graph.drop();
+        graph_rows_changed = true;
+      }
+      if (!use_graph || graph_rows_changed) {
+        step_eager(ds);
+        graph_rows_changed = false;
+      } else {
+        if (!graph.exec) ++captures;
+        graph.run(ds, [&] { step_eager(ds); });
+      }
+      ++passes;
+      row_steps += nrows;
+      ++k;
+      if (passes > pass_limit) throw std::runtime_error("generate: decode did not terminate");
+    }
+  } catch (...) {
+    graph.abort(ds);
+    throw;
+  }
+  if (use_graph) {
+    HIP_OK(hipEventRecord(e->ev_g1, ds));
+    HIP_OK(hipStreamWaitEvent(st, e->ev_g1, 0));
+  }
+  if (graph.exec) {
+    HIP_OK(hipStreamSynchronize(ds));
+    graph.drop();
+  }
+
+  // ---- results, by window
+  std::vector<int> res_tok((size_t)W * C), res_len(W);
+  std::vector<float> res_cum(W), res_ns(W), res_lp, res_lpo;
+  HIP_OK(hipMemcpyAsync(res_tok.data(), e->d_res_tok.p, res_tok.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(res_len.data(), e->d_res_len.p, (size_t)W * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(res_cum.data(), e->d_res_cum.p, (size_t)W * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(res_ns.data(), e->d_res_ns.p, (size_t)W * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+  if (rec) {
+    res_lp.resize((size_t)W * C);
+    res_lpo.resize((size_t)W * C);
+    HIP_OK(hipMemcpyAsync(res_lp.data(), e->d_res_lp.p, res_lp.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(res_lpo.data(), e->d_res_lp_o.p, res_lpo.size() * 4, hipMemcpyDeviceToHost, st));
+  }
+  HIP_OK(hipStreamSynchronize(st));
+  check_decode_error(h_cnt + 1);
+  const float lp = a->length_penalty;
+  for (int w = 0; w < W; ++w) {
+    const int n = res_len[w];
+    if (n < 0 || n > ML) throw std::runtime_error("generate: window " + std::to_string(w) + " has no result");
+    for (int i = 0; i < n; ++i) a->h_tokens[(size_t)w * ML + i] = res_tok[(size_t)w * C + i];
+    a->h_lengths[w] = n;
+    a->h_scores[w] = res_cum[w] / std::pow((float)std::max(n, 1), lp);
+    if (a->h_cum_logprob) a->h_cum_logprob[w] = res_cum[w];
+    if (a->h_no_speech) a->h_no_speech[w] = res_ns[w];
+    if (rec) {
+      const int nr = std::min(ML, n + (P + n < ML ? 1 : 0));
+      for (int i = 0; i < nr; ++i) {
+        a->h_token_logprobs[(size_t)w * ML + i] = res_lp[(size_t)w * C + i];
+        if (a->h_token_logprobs_other) a->h_token_logprobs_other[(size_t)w * ML + i] = res_lpo[(size_t)w * C + i];
+      }
+    }
+  }
+  if (a->h_steps) a->h_steps[0] = (int)passes;
+  if (a->h_stats) {
+    a->h_stats[0] = passes;
+    a->h_stats[1] = row_steps;
+    a->h_stats[2] = refills;
+    a->h_stats[3] = captures;
+  }
 }
 
 // logit_rows (optional): the pass rows whose logits are wanted, in output order (overrides last_only)
@@ -1265,7 +1686,7 @@ int guarded(wm_engine* e, F&& f) {
 extern "C" {
 
 const char* wm_last_error(void) { return g_err.c_str(); }
-int32_t wm_abi_version(void) { return 1; }
+int32_t wm_abi_version(void) { return 2; }
 
 int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
   try {
@@ -1344,7 +1765,9 @@ void wm_destroy(wm_engine* e) {
                     &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt, &e->d_lnstat,
                     &e->xenc, &e->xscale, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml, &e->a_logits, &e->a_attn,
                     &e->a_next, &e->a_probs, &e->a_rowsum, &e->a_z, &e->a_mat, &e->a_cost, &e->a_trace, &e->a_pi,
-                    &e->a_pj, &e->a_plen, &e->a_meta})
+                    &e->a_pj, &e->a_plen, &e->a_meta, &e->d_tok_lp, &e->d_tok_lp_o, &e->d_fin_lp, &e->d_win_prompt,
+                    &e->d_win_slot, &e->d_hyp_out, &e->d_res_tok, &e->d_res_len, &e->d_res_cum, &e->d_res_ns, &e->d_res_lp,
+                    &e->d_res_lp_o, &e->d_ev})
     b->release();
   if (e->st2) (void)hipStreamDestroy(e->st2);
   if (e->gst) (void)hipStreamDestroy(e->gst);
@@ -1477,6 +1900,24 @@ int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_
                int32_t last_only, const int32_t* h_align_heads, int32_t n_align, float* d_attn, void* stream) {
   return guarded(e, [&] {
     forward(e, n_seq, h_slots, seq_len, h_tokens, d_logits, last_only, h_align_heads, n_align, d_attn, (hipStream_t)stream);
+  });
+}
+
+int wm_detect_language(wm_engine* e, int32_t n, const int32_t* h_slots, int32_t lang_begin, int32_t n_langs,
+                       float* h_probs, void* stream) {
+  return guarded(e, [&] {
+    if (n <= 0) return;
+    if (lang_begin < 0 || n_langs <= 0 || lang_begin + n_langs > e->dm.n_vocab)
+      throw std::runtime_error("wm_detect_language: language tokens outside the vocabulary");
+    hipStream_t st = (hipStream_t)stream;
+    const int V = e->dm.n_vocab;
+    std::vector<int> toks(n, e->dm.sot);
+    e->a_logits.ensure((size_t)n * V * 4);
+    forward(e, n, h_slots, 1, toks.data(), e->a_logits.as<float>(), 1, nullptr, 0, nullptr, st);
+    e->a_probs.ensure((size_t)n * n_langs * 4);
+    launch_lang_probs(e->a_logits.as<float>(), V, n, lang_begin, n_langs, e->a_probs.as<float>(), st);
+    HIP_OK(hipMemcpyAsync(h_probs, e->a_probs.p, (size_t)n * n_langs * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
   });
 }
 
@@ -1616,7 +2057,46 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
         else { e->ckv.release(); e->xenc.release(); }
       }
     }
+    else if (k == "debug_nan_row") e->dbg_nan_row = (int)std::max<int64_t>(-1, std::min<int64_t>(value, 1 << 30));
     else throw std::runtime_error("wm_set_option: unknown option " + k);
+  });
+}
+
+int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
+  return guarded(e, [&] {
+    if (!key || !value) throw std::runtime_error("wm_get_option: null argument");
+    const std::string k(key);
+    auto proj = [&](size_t n) {
+      const std::string pj = k.substr(n);
+      for (int i = 0; i < DEC_NPROJ; ++i)
+        if (pj == kDecProjNames[i]) return i;
+      throw std::runtime_error("wm_get_option: unknown projection " + pj);
+    };
+    if (k == "decode_split") *value = e->dec_split;
+    else if (k == "decode_graph") *value = e->dec_graph;
+    else if (k == "decode_gemv") *value = e->dec_gemv;
+    else if (k == "decode_gemv_ln") *value = e->dec_gemv_ln;
+    else if (k == "decode_ring_gemm") *value = e->dec_ring;
+    else if (k == "decode_gemm_plan") {
+      int p = -1;
+      for (int q = 0; q < 2 && p < 0; ++q) {
+        bool eq = true;
+        for (int i = 0; i < DEC_NPROJ; ++i) eq &= e->dec_plan[i] == kDecPlanPresets[q][i] && e->dec_cols[i] == kDecColsPresets[q][i];
+        if (eq) p = q;
+      }
+      *value = p;                               // -1: a per-projection setting departs from both presets
+    } else if (k.rfind("decode_gemm.", 0) == 0) *value = e->dec_plan[proj(12)];
+    else if (k.rfind("decode_gemm_cols.", 0) == 0) *value = e->dec_cols[proj(17)];
+    else if (k == "cross_attn_blocks") *value = e->cross_cap;
+    else if (k == "cross_attn_fuse") *value = e->cross_fuse;
+    else if (k == "cross_attn_snake") *value = e->xsnake;
+    else if (k == "cross_attn_keep") *value = e->xkeep;
+    else if (k == "gemm_persistent") *value = gemm_8p_get_persistent();
+    else if (k == "encode_chunk") *value = e->enc_chunk;
+    else if (k == "cross_fp8") *value = e->cross_fp8;
+    else if (k == "cross_mode") *value = e->cross_mode;
+    else if (k == "debug_nan_row") *value = e->dbg_nan_row;
+    else throw std::runtime_error("wm_get_option: unknown option " + k);
   });
 }
 

@@ -64,6 +64,7 @@ void launch_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N, int
 // Large-M path, staggered 4-phase-per-K-tile schedule (gemm_8p.hip): used by launch_gemm when applicable.
 bool gemm_8p_applicable(int M, int N, int K);
 void gemm_8p_set_persistent(int on);
+int gemm_8p_get_persistent();
 void launch_gemm_8p(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, hipStream_t st);
 
 // Large-M path (gemm_big.hip): 256x128 tiles, LDS-DMA ring; used by launch_gemm when applicable.

@@ -559,6 +559,7 @@ static int g_gemm_persist = [] {
 }();
 static int gemm_8p_persistent() { return g_gemm_persist; }
 void gemm_8p_set_persistent(int on) { g_gemm_persist = on != 0; }
+int gemm_8p_get_persistent() { return g_gemm_persist; }
 
 static int device_cus() {
   static const int v = [] {

@@ -66,19 +66,23 @@ void launch_layernorm(const float* x, long long ldx, const int* row_idx, int row
 }
 
 // x[r, :] = E[tok[r], :] + P[pos[r], :]
-// Token ids and positions are clamped to the tables: a numerically broken step (NaN logits select no valid
-// token) then yields a wrong decode that the host reports, never an out-of-bounds read.
+// A token id or position outside its table is an error (reported through the decode's device error word, which
+// the host raises on); the index is also clamped, purely as a memory guard, so the broken row never reads out of
+// bounds before the host sees the error.
 __global__ void embed_kernel(const int* __restrict__ tok, const int* __restrict__ pos, const bf16* __restrict__ E,
-                             const float* __restrict__ P, float* __restrict__ x, int d, int n_vocab, int n_pos) {
+                             const float* __restrict__ P, float* __restrict__ x, int d, int n_vocab, int n_pos,
+                             int* __restrict__ err) {
   const int r = blockIdx.x;
-  const long long t = min(max(tok[r], 0), n_vocab - 1), p = min(max(pos[r], 0), n_pos - 1);
+  const int t0 = tok[r], p0 = pos[r];
+  if ((t0 < 0 || t0 >= n_vocab || p0 < 0 || p0 >= n_pos) && threadIdx.x == 0) wm_report_error(err, WM_ERR_TOKEN_RANGE, t0, p0);
+  const long long t = min(max(t0, 0), n_vocab - 1), p = min(max(p0, 0), n_pos - 1);
   for (int c = threadIdx.x; c < d; c += blockDim.x) x[(long long)r * d + c] = bf2f(E[t * d + c]) + P[p * d + c];
 }
 
 void launch_embed(const int* tok, const int* pos, const bf16* E, const float* P, float* x, int rows, int d, int n_vocab,
-                  int n_pos, hipStream_t st) {
+                  int n_pos, hipStream_t st, int* err) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(256), 0, st, tok, pos, E, P, x, d, n_vocab, n_pos);
+  hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(256), 0, st, tok, pos, E, P, x, d, n_vocab, n_pos, err);
   WM_LAUNCH_CHECK("embed_kernel");
 }
 

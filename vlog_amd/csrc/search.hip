@@ -65,14 +65,17 @@ __device__ float block_sum(float v, float* sh) {
 
 // MODE = p.mode as a template parameter (0 greedy, 1 beam top-k, 2 sampling): each instantiation only holds
 // the registers its mode needs next to the register-resident row.
-template <int MODE>
+// REC: also write the per-step records (p.tok_lp / p.tok_lp_other; an extra register pass for the best other
+// token), instantiated only when a caller asks for them.
+template <int MODE, bool REC>
 __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   __shared__ Cand sh_c[NW];
   __shared__ float sh_f[NW];
   __shared__ int s_info[4];
   __shared__ Cand s_top[NW * KMAX];
   __shared__ int s_last_ts;
-  const int h = blockIdx.x, tid = threadIdx.x;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int h = p.row_hyp ? p.row_hyp[row] : row;
   if (p.done[h]) return;
   const int len = p.seq_len[h];
   const int* seq = p.tokens + (long long)h * p.n_ctx;
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   }
   __syncthreads();
   const int first = s_info[0], pair_rule = s_info[1], bound = s_info[2];
-  const float* lg = p.logits + (long long)h * p.ldl;
+  const float* lg = p.logits + (long long)row * p.ldl;
   const int V = p.V;
   const bool ts_on = p.with_ts != 0;
   const unsigned long long sup = p.suppress_bits[tid];
@@ -184,6 +187,25 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   }
   st = block_sum(st, sh_f);
   ss = block_sum(ss, sh_f);
+  // Numeric breakage is an error, never a token: a NaN or +inf among the allowed logits makes its segment's
+  // exp-sum NaN (NaN, and inf - inf, propagate through the sums), and a row whose rules allow nothing leaves both
+  // maxima at -inf.  The hypothesis ends, the device error word records it, and the host raises at its next poll
+  // (the worker turns that into FAILED, worker/transcription.py:436-443).  All tested values are block-uniform.
+  if (isnan(st) || isnan(ss) || (mt.v == -INFINITY && ms.v == -INFINITY)) {
+    if (tid == 0) {
+      wm_report_error(p.err, (isnan(st) || isnan(ss)) ? WM_ERR_NONFINITE : WM_ERR_NO_TOKEN, h, len - p.sample_begin);
+      if (MODE == 1) {
+        for (int r = 0; r < p.topk; ++r) {
+          p.cand_tok[(long long)h * p.topk + r] = -1;
+          p.cand_lp[(long long)h * p.topk + r] = -INFINITY;
+        }
+      } else {
+        p.done[h] = 1;
+        atomicSub(p.n_active, 1);
+      }
+    }
+    return;
+  }
   const float lse_t = mt.v > -INFINITY ? mt.v + logf(st) : -INFINITY;
   const float lse_s = ms.v > -INFINITY ? ms.v + logf(ss) : -INFINITY;
   const bool forced = ts_on && lse_s > mt.v;
@@ -350,25 +372,71 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
     gt = block_argmax(gt, sh_c);
     gs = block_argmax(gs, sh_c);
   }
+  // the chosen token: every thread holds the block-reduced candidates and `forced`, so it is block-uniform
+  int tok;
+  if (MODE == 2) tok = forced ? gs.i : (better(gt.v, gt.i, gs.v, gs.i) ? gt.i : gs.i);
+  else tok = forced ? ms.i : (better(mt.v, mt.i, ms.v, ms.i) ? mt.i : ms.i);
+  float lp_other = -INFINITY;
+  if (REC) {
+    // the best allowed token other than the chosen one (the per-step margin of the records)
+    const unsigned long long avail = forced ? (live & ts_mask) : live;
+    Cand b{-INFINITY, 0x7fffffff};
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * SB;
+      if (((avail >> k) & 1) && i != tok && better(xat(k), i, b.v, b.i)) { b.v = xat(k); b.i = i; }
+    }
+    b = block_argmax(b, sh_c);
+    lp_other = b.v - Z;
+  }
+  __shared__ int s_fin;
   if (tid == 0) {
-    int tok;
-    if (MODE == 2) tok = forced ? gs.i : (better(gt.v, gt.i, gs.v, gs.i) ? gt.i : gs.i);
-    else tok = forced ? ms.i : (better(mt.v, mt.i, ms.v, ms.i) ? mt.i : ms.i);
     const float lp = lg[tok] - Z;
-    p.cum[h] += lp;
+    const float cum = p.cum[h] + lp;
+    p.cum[h] = cum;
+    if (REC && p.tok_lp) {
+      p.tok_lp[(long long)h * p.n_ctx + len] = lp;
+      if (p.tok_lp_other) p.tok_lp_other[(long long)h * p.n_ctx + len] = lp_other;
+    }
     bool fin = false;
     if (tok == p.eot) {
       fin = true;
     } else {
       p.tokens[(long long)h * p.n_ctx + len] = tok;
       p.seq_len[h] = len + 1;
-      p.row_tok[h] = tok;
-      p.row_pos[h] = len;
+      p.row_tok[row] = tok;
+      p.row_pos[row] = len;
       if (len + 1 >= p.max_length) fin = true;
     }
     if (fin) {
       p.done[h] = 1;
       atomicSub(p.n_active, 1);
+      if (p.res_tok) {
+        const int o = p.hyp_out[h];
+        p.res_len[o] = len + (tok == p.eot ? 0 : 1) - p.sample_begin;
+        p.res_cum[o] = cum;
+      }
+    }
+    s_fin = fin;
+  }
+  if (p.res_tok) {
+    // row-set decode: the hypothesis' slot is reused once it ends, so its tokens (and records) move to the
+    // output tables now, copied by the whole block
+    __syncthreads();
+    if (s_fin) {
+      const int o = p.hyp_out[h];
+      const int n = len + (tok == p.eot ? 0 : 1) - p.sample_begin;     // generated tokens, <|endoftext|> excluded
+      const int* src = p.tokens + (long long)h * p.n_ctx + p.sample_begin;
+      for (int t = tid; t < n; t += SB) p.res_tok[(long long)o * p.n_ctx + t] = src[t];
+      if (REC && p.tok_lp && p.res_lp) {
+        const int nr = len + 1 - p.sample_begin;                       // records up to position len
+        const float* a = p.tok_lp + (long long)h * p.n_ctx + p.sample_begin;
+        const float* b = p.tok_lp_other ? p.tok_lp_other + (long long)h * p.n_ctx + p.sample_begin : nullptr;
+        for (int t = tid; t < nr; t += SB) {
+          p.res_lp[(long long)o * p.n_ctx + t] = a[t];
+          if (b && p.res_lp_other) p.res_lp_other[(long long)o * p.n_ctx + t] = b[t];
+        }
+      }
     }
   }
 }
@@ -384,16 +452,64 @@ void search_suppress_bits(const unsigned char* sup, int V, unsigned long long* b
   }
 }
 
-void launch_logits_select(const SearchParams& p, int n_hyp, hipStream_t st) {
-  if (n_hyp <= 0) return;
+void launch_logits_select(const SearchParams& p, int n_rows, hipStream_t st) {
+  if (n_rows <= 0) return;
   if (p.V > 53248) throw std::runtime_error("logits_select: vocabulary larger than 53248");
   if (p.mode == 1 && (p.topk < 1 || p.topk > KMAX)) throw std::runtime_error("beam size must be <= 8");
-  switch (p.mode) {
-    case 0: hipLaunchKernelGGL(logits_select_kernel<0>, dim3(n_hyp), dim3(SB), 0, st, p); break;
-    case 1: hipLaunchKernelGGL(logits_select_kernel<1>, dim3(n_hyp), dim3(SB), 0, st, p); break;
-    default: hipLaunchKernelGGL(logits_select_kernel<2>, dim3(n_hyp), dim3(SB), 0, st, p); break;
+  if (p.res_tok && (!p.hyp_out || !p.res_len || !p.res_cum || p.mode == 1))
+    throw std::runtime_error("logits_select: incomplete output tables");
+  const bool rec = p.tok_lp != nullptr && p.mode != 1;     // beam: beam_select_kernel keeps the records
+  const dim3 g(n_rows), b(SB);
+  switch (p.mode * 2 + (rec ? 1 : 0)) {
+    case 0: hipLaunchKernelGGL((logits_select_kernel<0, false>), g, b, 0, st, p); break;
+    case 1: hipLaunchKernelGGL((logits_select_kernel<0, true>), g, b, 0, st, p); break;
+    case 2: case 3: hipLaunchKernelGGL((logits_select_kernel<1, false>), g, b, 0, st, p); break;
+    case 4: hipLaunchKernelGGL((logits_select_kernel<2, false>), g, b, 0, st, p); break;
+    default: hipLaunchKernelGGL((logits_select_kernel<2, true>), g, b, 0, st, p); break;
   }
   WM_LAUNCH_CHECK("logits_select_kernel");
+}
+
+// ------------------------------------------------------------------------------------ row-set bookkeeping
+__global__ __launch_bounds__(256) void hyp_start_kernel(const int* __restrict__ hs, const int* __restrict__ ws,
+                                                        const int* __restrict__ win_prompt, int P,
+                                                        const int* __restrict__ win_slot, int n_ctx, int* tokens,
+                                                        int* seq_len, int* done, float* cum, int* hyp_slot, int* hyp_out) {
+  const int h = hs[blockIdx.x], w = ws[blockIdx.x];
+  for (int p = threadIdx.x; p < P; p += blockDim.x) tokens[(long long)h * n_ctx + p] = win_prompt[(long long)w * P + p];
+  if (threadIdx.x == 0) {
+    seq_len[h] = P;
+    done[h] = 0;
+    cum[h] = 0.f;
+    hyp_slot[h] = win_slot[w];
+    hyp_out[h] = w;
+  }
+}
+
+void launch_hyp_start(int n, const int* hs, const int* ws, const int* win_prompt, int P, const int* win_slot, int n_ctx,
+                      int* tokens, int* seq_len, int* done, float* cum, int* hyp_slot, int* hyp_out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(hyp_start_kernel, dim3(n), dim3(64), 0, st, hs, ws, win_prompt, P, win_slot, n_ctx, tokens, seq_len,
+                     done, cum, hyp_slot, hyp_out);
+  WM_LAUNCH_CHECK("hyp_start_kernel");
+}
+
+__global__ __launch_bounds__(256) void rows_fill_kernel(int n, const int* __restrict__ src, int* __restrict__ tok,
+                                                        int* __restrict__ pos, const int* __restrict__ row_tok,
+                                                        const int* __restrict__ row_pos) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = src[i];
+  if (s >= 0) {
+    tok[i] = row_tok[s];
+    pos[i] = row_pos[s];
+  }
+}
+
+void launch_rows_fill(int n, const int* src, int* tok, int* pos, const int* row_tok, const int* row_pos, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(rows_fill_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, src, tok, pos, row_tok, row_pos);
+  WM_LAUNCH_CHECK("rows_fill_kernel");
 }
 
 // ------------------------------------------------------------------------------------ beam bookkeeping
@@ -409,10 +525,11 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
   constexpr int NC = BMAX * (BMAX + 1);
   __shared__ int s_tok[BMAX][448];
   __shared__ int s_lin[BMAX][448];
+  __shared__ float s_lp[BMAX][448];          // per-step records (p.tok_lp)
   __shared__ float c_sc[NC], o_sc[NC];
   __shared__ int c_ok[NC], o_src[NC], o_tk[NC];
   __shared__ int s_par[BMAX], s_new[BMAX];
-  __shared__ float s_sc[BMAX];
+  __shared__ float s_sc[BMAX], s_cum[BMAX];
   __shared__ int f_src[CMAX], f_slot[CMAX];
   __shared__ float f_sc[CMAX];
   __shared__ int s_nlive, s_nf_new;
@@ -420,10 +537,12 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
   const int K = p.beam, h0 = w * K, T = K + 1, NK = K * T;
   if (p.done[h0]) return;
   const int len = p.seq_len[h0];
+  const bool rec = p.tok_lp != nullptr;
   for (int i = tid; i < K * len; i += blockDim.x) {
     const int b = i / len, t = i - b * len;
     s_tok[b][t] = p.tokens[(long long)(h0 + b) * p.n_ctx + t];
     s_lin[b][t] = p.lin[(long long)(h0 + b) * p.n_ctx + t];
+    if (rec) s_lp[b][t] = p.tok_lp[(long long)(h0 + b) * p.n_ctx + t];
   }
   // candidate i = (beam j, rank r) in (beam, rank) order
   float sc_i = -INFINITY;
@@ -431,9 +550,13 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
   if (tid < NK) {
     const int j = tid / T;
     const float c = p.cum[h0 + j];
+    if (tid % T == 0) s_cum[j] = c;
     tk_i = p.cand_tok[(long long)h0 * T + tid];
-    const bool ok = c != -INFINITY && tk_i >= 0;
-    if (ok) sc_i = c + p.cand_lp[(long long)h0 * T + tid];
+    const float s = c + p.cand_lp[(long long)h0 * T + tid];
+    // a NaN score would compare false against every other and break the ranks' total order (the select kernel
+    // already reports non-finite rows and emits no candidate for them; this keeps the ranking well-formed)
+    const bool ok = c != -INFINITY && tk_i >= 0 && !isnan(s);
+    if (ok) sc_i = s;
     c_ok[tid] = ok;
     c_sc[tid] = sc_i;
   }
@@ -475,10 +598,12 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
     for (int i = tid; i < nnew * ng; i += blockDim.x) {
       const int f = i / ng, t = i - f * ng;
       p.fin_tok[((long long)w * p.max_cand + f_slot[f]) * p.n_ctx + t] = s_tok[f_src[f]][p.sample_begin + t];
+      if (rec) p.fin_lp[((long long)w * p.max_cand + f_slot[f]) * p.n_ctx + t] = s_lp[f_src[f]][p.sample_begin + t];
     }
     if (tid < nnew) {
       p.fin_len[w * p.max_cand + f_slot[tid]] = ng;
       p.fin_cum[w * p.max_cand + f_slot[tid]] = f_sc[tid];
+      if (rec) p.fin_lp[((long long)w * p.max_cand + f_slot[tid]) * p.n_ctx + ng] = f_sc[tid] - s_cum[f_src[tid]];
     }
   }
   const int nlive = s_nlive;
@@ -488,12 +613,14 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
     const int par = b < nlive ? s_par[b] : s_par[0];
     p.tokens[(long long)(h0 + b) * p.n_ctx + t] = s_tok[par][t];
     p.lin[(long long)(h0 + b) * p.n_ctx + t] = s_lin[par][t];
+    if (rec) p.tok_lp[(long long)(h0 + b) * p.n_ctx + t] = s_lp[par][t];
   }
   __syncthreads();
   if (tid < K) {
     const int b = tid;
     const int par = b < nlive ? s_par[b] : s_par[0];
     const int tok = b < nlive ? s_new[b] : s_new[0];
+    if (rec) p.tok_lp[(long long)(h0 + b) * p.n_ctx + len] = b < nlive ? s_sc[b] - s_cum[par] : -INFINITY;
     p.tokens[(long long)(h0 + b) * p.n_ctx + len] = tok;
     p.lin[(long long)(h0 + b) * p.n_ctx + len] = h0 + b;      // the next step writes KV at (hyp, len)
     p.seq_len[h0 + b] = len + 1;
@@ -511,9 +638,38 @@ void launch_beam_select(const BeamParams& p, int n_win, hipStream_t st) {
   WM_LAUNCH_CHECK("beam_select_kernel");
 }
 
+// Language detection: out[r][j] = softmax over logits[r][lang_begin .. lang_begin + n_langs) (ctranslate2
+// Whisper.detect_language's probabilities [FW↑]), f32 with an f32 max / sum
+__global__ __launch_bounds__(256) void lang_probs_kernel(const float* __restrict__ logits, long long ldl, int lang_begin,
+                                                         int n_langs, float* __restrict__ out) {
+  __shared__ float sh[4];
+  const float* lg = logits + (long long)blockIdx.x * ldl + lang_begin;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float m = -INFINITY;
+  for (int j = tid; j < n_langs; j += 256) m = fmaxf(m, lg[j]);
+  m = wave_max(m);
+  if (lane == 0) sh[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int j = tid; j < n_langs; j += 256) s += expf(lg[j] - m);
+  s = wave_sum(s);
+  if (lane == 0) sh[wv] = s;
+  __syncthreads();
+  s = sh[0] + sh[1] + sh[2] + sh[3];
+  for (int j = tid; j < n_langs; j += 256) out[(long long)blockIdx.x * n_langs + j] = expf(lg[j] - m) / s;
+}
+
+void launch_lang_probs(const float* logits, long long ldl, int rows, int lang_begin, int n_langs, float* out, hipStream_t st) {
+  if (rows <= 0 || n_langs <= 0) return;
+  hipLaunchKernelGGL(lang_probs_kernel, dim3(rows), dim3(256), 0, st, logits, ldl, lang_begin, n_langs, out);
+  WM_LAUNCH_CHECK("lang_probs_kernel");
+}
+
 // softmax(logits[r])[no_speech]
 __global__ __launch_bounds__(SB) void no_speech_kernel(const float* __restrict__ logits, long long ldl, int V, int ns,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out, const int* __restrict__ out_idx) {
   __shared__ Cand sh_c[NW];
   __shared__ float sh_f[NW];
   const float* lg = logits + (long long)blockIdx.x * ldl;
@@ -524,11 +680,12 @@ __global__ __launch_bounds__(SB) void no_speech_kernel(const float* __restrict__
   float s = 0.f;
   for (int i = threadIdx.x; i < V; i += SB) s += expf(lg[i] - m.v);
   s = block_sum(s, sh_f);
-  if (threadIdx.x == 0) out[blockIdx.x] = expf(lg[ns] - m.v) / s;
+  if (threadIdx.x == 0) out[out_idx ? out_idx[blockIdx.x] : blockIdx.x] = expf(lg[ns] - m.v) / s;
 }
 
-void launch_no_speech(const float* logits, long long ldl, int V, int rows, int no_speech, float* out, hipStream_t st) {
+void launch_no_speech(const float* logits, long long ldl, int V, int rows, int no_speech, float* out, hipStream_t st,
+                      const int* out_idx) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(no_speech_kernel, dim3(rows), dim3(SB), 0, st, logits, ldl, V, no_speech, out);
+  hipLaunchKernelGGL(no_speech_kernel, dim3(rows), dim3(SB), 0, st, logits, ldl, V, no_speech, out, out_idx);
   WM_LAUNCH_CHECK("no_speech_kernel");
 }

@@ -30,6 +30,10 @@ class GenResult:
     score: float
     cum_logprob: float
     no_speech_prob: float
+    # per-step records (generate(record_logprobs=True)): log-prob of the token chosen at each step, the final
+    # <|endoftext|> included when the window ended on it; greedy / sampling also the best other allowed token's
+    token_logprobs: Optional[np.ndarray] = None
+    token_logprobs_other: Optional[np.ndarray] = None
 
 
 def pack_weights(dims: ModelDims, sd: Dict[str, torch.Tensor], device) -> Dict[str, torch.Tensor]:
@@ -101,7 +105,6 @@ class GpuEngine:
     def __init__(self, dims: ModelDims, state_dict: Dict[str, torch.Tensor], device_index: int = 0):
         self.lib = _capi.load()
         self.dims = dims
-        self._opts: Dict[str, int] = {}
         self.device = torch.device("cuda", device_index)
         st = dims.specials
         cd = _capi.ModelDimsC(dims.n_mels, dims.n_state, dims.n_head, dims.n_enc_layer, dims.n_dec_layer,
@@ -180,11 +183,16 @@ class GpuEngine:
     def set_option(self, key: str, value: int) -> None:
         """Engine scheduling knob (wm_set_option), e.g. set_option("decode_split", 0)."""
         _capi.check(self.lib.wm_set_option(self.h, key.encode(), int(value)), "wm_set_option")
-        self._opts[key] = int(value)
 
     def option(self, key: str, default: Optional[int] = None) -> Optional[int]:
-        """The last value set through set_option (None / default when never set: the engine default)."""
-        return self._opts.get(key, default)
+        """The engine's current value of an option (wm_get_option: includes environment overrides and defaults);
+        `default` only for keys the engine does not know."""
+        v = C.c_int64()
+        if self.lib.wm_get_option(self.h, key.encode(), C.byref(v)) != 0:
+            if default is not None:
+                return default
+            _capi.check(-1, f"wm_get_option({key})")
+        return int(v.value)
 
     def device_bytes(self) -> int:
         return int(self.lib.wm_device_bytes(self.h))
@@ -267,7 +275,11 @@ class GpuEngine:
                  temperature: float = 0.0, num_hypotheses: int = 1, seed: int = 0,
                  suppress_tokens: Sequence[int] = (), suppress_blank: bool = True,
                  max_initial_timestamp_index: Optional[int] = 50, with_timestamps: bool = True,
-                 sot_index: Optional[int] = None, check_every: int = 4) -> Tuple[List[GenResult], int]:
+                 sot_index: Optional[int] = None, check_every: int = 4, max_rows: int = 0, compact: bool = False,
+                 record_logprobs: bool = False, stats: Optional[dict] = None) -> Tuple[List[GenResult], int]:
+        """ctranslate2 Whisper.generate over windows in slots (wm_generate).  max_rows / compact: the row-set decode
+        (greedy / one sampled hypothesis; windows refill finished rows in the given order, include/whisper_mi355.h).
+        record_logprobs: per-step log-prob records in each GenResult.  stats: filled with the decode's counters."""
         W = len(slots)
         P = len(prompts[0])
         if any(len(p) != P for p in prompts):
@@ -286,14 +298,29 @@ class GpuEngine:
         cum = np.zeros(W, dtype=np.float32)
         ns = np.zeros(W, dtype=np.float32)
         steps = np.zeros(1, dtype=np.int32)
+        lp = np.full((W, max_length), np.nan, dtype=np.float32) if record_logprobs else None
+        lpo = np.full((W, max_length), np.nan, dtype=np.float32) if record_logprobs else None
+        st64 = np.zeros(4, dtype=np.int64)
         a = _capi.GenerateArgsC(
             W, _i32p(h_slots), P, _i32p(h_prompts), sot_index, beam_size, patience, length_penalty, max_length,
             temperature, num_hypotheses, seed, _i32p(sup), int(sup.size), int(bool(suppress_blank)),
             -1 if max_initial_timestamp_index is None else int(max_initial_timestamp_index), int(bool(with_timestamps)),
-            check_every, _i32p(toks), _i32p(lens), _f32p(scores), _f32p(cum), _f32p(ns), _i32p(steps))
+            check_every, _i32p(toks), _i32p(lens), _f32p(scores), _f32p(cum), _f32p(ns), _i32p(steps),
+            int(max_rows), int(bool(compact)), _f32p(lp) if lp is not None else None,
+            _f32p(lpo) if lpo is not None else None, st64.ctypes.data_as(C.POINTER(C.c_int64)))
         with torch.cuda.device(self.device):
             _capi.check(self.lib.wm_generate(self.h, C.byref(a), self.stream_ptr()), "wm_generate")
-        res = [GenResult(toks[w, : lens[w]].tolist(), float(scores[w]), float(cum[w]), float(ns[w])) for w in range(W)]
+        res = []
+        for w in range(W):
+            n = int(lens[w])
+            r = GenResult(toks[w, :n].tolist(), float(scores[w]), float(cum[w]), float(ns[w]))
+            if lp is not None:
+                nr = min(max_length, n + (1 if P + n < max_length else 0))
+                r.token_logprobs = lp[w, :nr].copy()
+                r.token_logprobs_other = lpo[w, :nr].copy()
+            res.append(r)
+        if stats is not None:
+            stats.update(passes=int(st64[0]), row_steps=int(st64[1]), refills=int(st64[2]), graph_captures=int(st64[3]))
         return res, int(steps[0])
 
     def forward(self, slots: Sequence[int], tokens: np.ndarray, last_only: bool = False,
@@ -315,6 +342,16 @@ class GpuEngine:
                                             C.c_void_p(attn.data_ptr()) if attn is not None else None,
                                             self.stream_ptr()), "wm_forward")
         return logits, attn
+
+    def detect_language(self, slots: Sequence[int], lang_begin: int, n_langs: int) -> np.ndarray:
+        """wm_detect_language: language-token probabilities [len(slots), n_langs] of one decoder step from
+        <|startoftranscript|> per window (softmax on the device)."""
+        h_slots = np.ascontiguousarray(slots, dtype=np.int32)
+        probs = np.zeros((len(slots), n_langs), dtype=np.float32)
+        with torch.cuda.device(self.device):
+            _capi.check(self.lib.wm_detect_language(self.h, len(slots), _i32p(h_slots), lang_begin, n_langs, _f32p(probs),
+                                                    self.stream_ptr()), "wm_detect_language")
+        return probs
 
     def align(self, slot: int, sot_sequence: Sequence[int], text_tokens: Sequence[int], num_frames: int,
               alignment_heads: Sequence[Tuple[int, int]], median_filter_width: int = 7):

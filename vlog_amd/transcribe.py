@@ -264,9 +264,7 @@ class WhisperModel:
                     break
                 size = max(0, min(N_FRAMES, content - seek))
                 self._encode(features, seek, size, 0)
-                logits, _ = self.engine.forward([0], np.array([[st.sot]], dtype=np.int32), last_only=True)
-                lg = logits[0, st.lang_begin: st.lang_begin + st.n_langs].double()
-                p = torch.softmax(lg, dim=0).cpu().numpy()
+                p = self.engine.detect_language([0], st.lang_begin, st.n_langs)[0]
                 order = np.argsort(-p, kind="stable")
                 all_probs = [(st.lang_codes[j], float(p[j])) for j in order]
                 lang, prob = all_probs[0]
