@@ -65,3 +65,64 @@ def test_gates_f32_vs_bf16_oracle(tiny):
     g = gate_windows(o16, lambda ws: enc[ws], prompt, res, dims.specials, opt, tok)
     assert_gates(g)
     assert g["identical"] == W and g["min_margin_identical_nats"] > 5.0, g
+
+
+# ------------------------------------------------------------------------------ variable-length plant (margin_var)
+@pytest.fixture(scope="module")
+def tiny_var():
+    from vlog_amd.weights import plant_margin
+    dims = model_dims("tiny")
+    sd = synthetic_state_dict(dims, seed=0)
+    plan = plant_margin(sd, dims, 0, variable=True)
+    w = round_bf16(sd)
+    o32 = OracleWhisper(w, dims, np.float32)
+    o16 = OracleWhisper(w, dims, np.float32, bf16_acts=True)
+    # windows of the corpus with levels from 8 to -4 (measured): one token to ~150
+    seeds = [10, 0, 3, 4, 12, 1, 2]
+    x = np.concatenate([speech_like(30.0, s) for s in seeds])
+    n = len(seeds)
+    mel = omel.log_mel(x, dims.n_mels)[:, :3000 * n].reshape(dims.n_mels, n, 3000).transpose(1, 0, 2)
+    enc = o32.encode(np.ascontiguousarray(mel))
+    tok = Tokenizer(dims, language="en")
+    prompt = list(tok.sot_sequence)
+    opt = GenerateOptions(suppress_tokens=list(tok.suppressed_tokens([-1])), max_length=448)
+    res = [generate_one(o32, o32.cross_kv(enc[i:i + 1]), prompt, dims.specials, opt) for i in range(n)]
+    return dims, plan, o16, enc, tok, prompt, opt, res
+
+
+def test_variable_length_follows_the_window_level(tiny_var):
+    """The script ends after the first exit timestamp whose threshold the window's level exceeds: lengths from
+    1 token to the whole script, each an exact prefix of the planted script (+ its timestamp pairs)."""
+    from vlog_amd.weights import LEVEL_W
+    dims, plan, _, enc, _, _, _, res = tiny_var
+    c, cr = plan.bit_channels
+    lengths = []
+    for i, r in enumerate(res):
+        s = np.sign((enc[i][:, c] - enc[i][:, cr]).mean(0))[:6]
+        L = int(sum(w * b for w, b in zip(LEVEL_W, s)))
+        k_exit = next((k for k, T in plan.exits if L > T), len(plan.slots) - 1)
+        flat, k, pos = list(r.tokens), 0, 0
+        while True:                                   # walk the script up to the exit slot
+            slot, kind = plan.slots[k], plan.kinds[k]
+            assert flat[pos] in slot, (i, pos, flat[pos], slot)
+            pos += 1
+            if k == k_exit:
+                break
+            if kind == "ts" and k > 0:
+                assert flat[pos] == flat[pos - 1]      # the timestamp pair
+                pos += 1
+            k += 1
+        assert pos == len(flat), (i, L, pos, len(flat))
+        assert r.score > -1e-3
+        lengths.append((L, len(flat)))
+    # a higher level ends earlier; the levels of these windows span one token to ~150+
+    by_level = sorted(lengths, key=lambda t: -t[0])
+    assert all(a[1] < b[1] for a, b in zip(by_level, by_level[1:]) if a[0] > b[0]), lengths
+    assert by_level[0][1] <= 5 and by_level[-1][1] >= 140, lengths
+
+
+def test_variable_length_gates_f32_vs_bf16_oracle(tiny_var):
+    dims, _, o16, enc, tok, prompt, opt, res = tiny_var
+    g = gate_windows(o16, lambda ws: enc[ws], prompt, res, dims.specials, opt, tok)
+    assert_gates(g)
+    assert g["identical"] == len(res) and g["min_margin_identical_nats"] > 5.0, g

@@ -27,7 +27,7 @@ import hashlib
 import json
 import math
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -100,8 +100,8 @@ def synthetic_state_dict(dims: ModelDims, seed: int = 0, eot_after: Optional[int
         else:
             t = std * torch.randn(shape, generator=g)
         sd[name] = t.float()
-    if plant == "margin":
-        plant_margin(sd, dims, seed)
+    if plant in ("margin", "margin_var"):
+        plant_margin(sd, dims, seed, variable=plant == "margin_var")
     elif plant is not None:
         raise ValueError(f"unknown plant {plant!r}")
     elif eot_after is not None:
@@ -169,12 +169,30 @@ class MarginPlan:
     kinds: List[str]
     bits: List[Optional[int]]
     first_key: Tuple[int, ...]          # prompt tokens whose unit emits slot 0 (the first timestamp)
+    # encoder output channels carrying the window bits (bit j = E[c_ch[j]] - E[c_ref[j]]), set by plant_margin
+    bit_channels: Optional[Tuple[List[int], List[int]]] = None
+    # variable-length script (plant "margin_var"): (slot k of a timestamp, threshold T) — the window ends with
+    # <|endoftext|> right after that timestamp when its level L = sum_j LEVEL_W[j] * bit_j exceeds T (first such k)
+    exits: List[Tuple[int, int]] = field(default_factory=list)
 
 
-def margin_plan(dims: ModelDims, seed: int = 0, n_segments: int = 8) -> MarginPlan:
+# Variable-length script (plant "margin_var"): 16 segments (up to ~225 tokens), level weights of the six bits (bit 0,
+# the corpus' first principal component = the window's mean log-mel energy, i.e. how much of it is speech, weighs
+# 3 and with a negative sign: more speech -> a lower level -> a later exit), and the exits: (segment whose end
+# timestamp may end the window (-1: the first timestamp), threshold).  Levels L in {-8, ..., 8} step 2 follow a
+# shifted binomial; thresholds sit at odd values, so every decision has a full level of margin:
+#   L = 8 -> 1 token, 6 -> ~2 segments, 4 -> 4, 2 -> 6, 0 -> 7, -2 -> 9, -4 -> 11, -6 -> 13, -8 -> all 16.
+VAR_SEGMENTS = 16
+LEVEL_W = (-3, 1, 1, 1, 1, 1)
+VAR_EXITS = ((-1, 7), (1, 5), (3, 3), (5, 1), (6, -1), (8, -3), (10, -5), (12, -7))
+
+
+def margin_plan(dims: ModelDims, seed: int = 0, n_segments: int = 8, variable: bool = False) -> MarginPlan:
     st = dims.specials
+    if variable:
+        n_segments = VAR_SEGMENTS
     rng = np.random.default_rng(int.from_bytes(hashlib.sha256(f"{seed}:margin_plan".encode()).digest()[:8], "little"))
-    text_ids = rng.choice(np.arange(1000, st.eot - 1000), size=400, replace=False).tolist()
+    text_ids = rng.choice(np.arange(1000, st.eot - 1000), size=400 if not variable else 800, replace=False).tolist()
     slots: List[Tuple[int, ...]] = [(st.timestamp_begin,)]
     kinds, bits = ["ts"], [None]
     span = 28.0 / n_segments
@@ -196,7 +214,7 @@ def margin_plan(dims: ModelDims, seed: int = 0, n_segments: int = 8) -> MarginPl
             slots.append((st.timestamp_begin + a,))
             kinds.append("ts_final")
             bits.append(None)
-        elif m % 2 == 1:                                 # a segment boundary that moves with the audio
+        elif m % 2 == 1 and not variable:                # a segment boundary that moves with the audio
             slots.append((st.timestamp_begin + a, st.timestamp_begin + a + 8))
             kinds.append("ts")
             bits.append(bit % N_BITS)
@@ -206,10 +224,14 @@ def margin_plan(dims: ModelDims, seed: int = 0, n_segments: int = 8) -> MarginPl
             kinds.append("ts")
             bits.append(None)
     first_key = (st.transcribe,) if dims.multilingual else (st.sot,)
-    return MarginPlan(slots, kinds, bits, first_key)
+    plan = MarginPlan(slots, kinds, bits, first_key)
+    if variable:
+        ends = [k for k, kd in enumerate(kinds) if kd in ("ts", "ts_final") and k > 0]     # segment m ends at ends[m]
+        plan.exits = [(0 if m < 0 else ends[m], t) for m, t in VAR_EXITS]
+    return plan
 
 
-def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) -> MarginPlan:
+def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, variable: bool = False) -> MarginPlan:
     """Plant a decisive, audio-dependent decoder program into seeded random weights (test model for the
     north_star token-identity / WER / timestamp gates).
 
@@ -230,11 +252,20 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
       a bit direction; a branch slot's two tokens differ by +-alpha times that direction, so the bit's sign
       picks the token (and segment boundaries move with it).
     The encoder channel trick: bit channel m and its reference m' receive identical (zero) writes from every
-    random layer and share LayerNorm affines, so E[m] - E[m'] is the planted value alone."""
+    random layer and share LayerNorm affines, so E[m] - E[m'] is the planted value alone.
+
+    variable=True (plant "margin_var", margin_plan VAR_*): a 16-segment script whose length follows the audio.  A
+    seventh, constant bit (+1 for every window) rides the same channels and head, so every bit the decoder reads is
+    s_j * rho_w with ONE common per-window scale rho_w; the window's level L = sum_j LEVEL_W[j] s_j is compared with a
+    threshold T as rho_w (L - T), whose sign is exact.  At each exit timestamp k, two units of decoder layer 2's MLP
+    key on that position (the repeat + next-text directions the successor table writes there) and differ only by
+    the level term: A = GELU(P + g (L - T) rho_w), B = GELU(P); A - B writes <|endoftext|>, so the window ends
+    after timestamp k iff L > T (GELU is monotonic where B sits), by a margin of one level (thousands of nats at
+    large-v3); elsewhere both units are off."""
     d, H = dims.n_state, dims.n_head
     hd = d // H
     st = dims.specials
-    plan = margin_plan(dims, seed)
+    plan = margin_plan(dims, seed, variable=variable)
     g = _gen(seed, "plant_margin")
     rng = np.random.default_rng(int.from_bytes(hashlib.sha256(f"{seed}:plant_margin".encode()).digest()[:8], "little"))
 
@@ -242,6 +273,10 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
     nb = N_BITS
     ch = rng.choice(d, size=6 * nb, replace=False)
     s_ch, s_ref, m_ch, m_ref, c_ch, c_ref = (ch[i * nb:(i + 1) * nb] for i in range(6))
+    k_ch = k_ref = None
+    if variable:
+        rng_v = np.random.default_rng(int.from_bytes(hashlib.sha256(f"{seed}:plant_margin_var".encode()).digest()[:8], "little"))
+        k_ch, k_ref = (int(c) for c in rng_v.choice(np.setdiff1d(np.arange(d), ch), size=2, replace=False))
     cal = _margin_calib(dims.n_mels)
     P = torch.tensor(cal["proj"], dtype=torch.float32)               # [n_mels, nb]
     med, fstd = cal["median"], cal["frame_std"]
@@ -251,6 +286,9 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
     c1w, c1b = sd["model.encoder.conv1.weight"], sd["model.encoder.conv1.bias"]       # [d, n_mels, 3]
     c2w, c2b = sd["model.encoder.conv2.weight"], sd["model.encoder.conv2.bias"]       # [d, d, 3]
     gelu_b1 = float(0.5 * b1 * (1.0 + math.erf(b1 / math.sqrt(2.0))))
+    if variable:                                         # the constant bit's channels: no stem writes either
+        for c in (k_ch, k_ref):
+            c1w[c] = 0.0; c1b[c] = 0.0; c2w[c] = 0.0; c2b[c] = 0.0
     for j in range(nb):
         for c in (s_ch[j], s_ref[j], m_ch[j], m_ref[j], c_ch[j], c_ref[j]):
             c1w[c] = 0.0; c1b[c] = 0.0; c2w[c] = 0.0; c2b[c] = 0.0
@@ -263,6 +301,8 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
         c2b[s_ref[j]] = b1 - gelu_b1
     pos = sd["model.encoder.embed_positions.weight"]
     pos[:, torch.as_tensor(ch)] = 0.0
+    if variable:
+        pos[:, [k_ch, k_ref]] = 0.0
     # layer 0, head h_e: uniform attention (q = 0) averaging (LN[s] - LN[s']) into channel m
     h_e = 0
     p0 = "model.encoder.layers.0.self_attn."
@@ -280,7 +320,7 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
     ln0w, ln0b = sd["model.encoder.layers.0.self_attn_layer_norm.weight"], sd["model.encoder.layers.0.self_attn_layer_norm.bias"]
     ln0w[torch.as_tensor(s_ref)] = ln0w[torch.as_tensor(s_ch)]
     ln0b[torch.as_tensor(s_ref)] = ln0b[torch.as_tensor(s_ch)]
-    prot = torch.as_tensor(np.concatenate([m_ch, m_ref, c_ch, c_ref]))
+    prot = torch.as_tensor(np.concatenate([m_ch, m_ref, c_ch, c_ref] + ([[k_ch, k_ref]] if variable else [])))
     for i in range(dims.n_enc_layer):
         p = f"model.encoder.layers.{i}."
         for w in ("self_attn.out_proj", "fc2"):
@@ -313,15 +353,31 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
         f2w[c_ch[j], 2 * j + 1] = -o_half / s_g
         f2b[c_ch[j]] = -o_half
     same_affine("model.encoder.layer_norm", c_ch, c_ref)
+    if variable:
+        # the constant bit: two units with fixed pre-activations s(2 + 1), s(2 - 1) (clip(2) = +1 exactly), and every
+        # carrying channel with a unit final-LayerNorm affine, so all seven bits leave the encoder as s_j * rho_w
+        # with one common per-window scale rho_w = o_half * mean_t rstd_t
+        for u, b in ((2 * nb, 3.0 * s_g), (2 * nb + 1, 1.0 * s_g)):
+            f1w[u] = 0.0
+            f1b[u] = b
+            f2w[:, u] = 0.0
+        f2w[k_ch, 2 * nb] = o_half / s_g
+        f2w[k_ch, 2 * nb + 1] = -o_half / s_g
+        f2b[k_ch] = -o_half
+        lnw, lnb = sd["model.encoder.layer_norm.weight"], sd["model.encoder.layer_norm.bias"]
+        carry = torch.as_tensor(np.concatenate([c_ch, c_ref, [k_ch, k_ref]]))
+        lnw[carry] = 1.0
+        lnb[carry] = 0.0
 
     # ---- decoder: orthonormal directions
     slot_dirs = len(plan.slots)
-    n_dirs = slot_dirs + nb + 4
+    n_dirs = slot_dirs + nb + 4 + (1 if variable else 0)
     q, _ = torch.linalg.qr(torch.randn(d, n_dirs, generator=g, dtype=torch.float64))
     V = q.T.float()                                      # rows: unit, mutually orthogonal
     v_slot = V[:slot_dirs]
     v_bit = V[slot_dirs: slot_dirs + nb]
     v_sot, v_en, v_eot, v_task = V[slot_dirs + nb: slot_dirs + nb + 4]
+    v_const = V[slot_dirs + nb + 4] if variable else None
     N = _resid_std(dims.n_dec_layer) * math.sqrt(d)     # norm of the random residual at the final LayerNorm
     R = 6.0 * N                                         # planted token embedding norm
     Bn = 5.0 * R                                        # successor write (> alpha * the largest bit term)
@@ -354,6 +410,10 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
         sd[pc + "v_proj.weight"][h_d * hd + j, c_ch[j]] = 1.0
         sd[pc + "v_proj.weight"][h_d * hd + j, c_ref[j]] = -1.0
         sd[pc + "out_proj.weight"][:, h_d * hd + j] = S_d * v_bit[j]
+    if variable:
+        sd[pc + "v_proj.weight"][h_d * hd + nb, k_ch] = 1.0
+        sd[pc + "v_proj.weight"][h_d * hd + nb, k_ref] = -1.0
+        sd[pc + "out_proj.weight"][:, h_d * hd + nb] = S_d * v_const
     # layer-0 MLP successor table
     pm = "model.decoder.layers.0."
     fc1w, fc1b = sd[pm + "fc1.weight"], sd[pm + "fc1.bias"]
@@ -378,6 +438,54 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0) ->
         fc1w[u] = gam * key
         fc1b[u] = -theta
         fc2w[:, u] = Bn * write / a_ref
+    if variable:
+        # Exits, in two stages (decoder layers 2 and 3; unit LayerNorm affines there so the keys read undistorted).
+        # Layer 2: per exit e, the window's level test as a saturated clip into its own direction,
+        #   I_e = +-o_I (sign of rho_w (L - T_e), exact: the threshold rides the constant bit),
+        # the same at every position; it also writes a ballast M along v_ball, which layer 3's fc2 bias removes, so
+        # layer 3's LayerNorm sees |x| ~ M at every position whatever the bit magnitudes (the position keys below are
+        # then calibrated for every model width).  Layer 3: per exit two units keyed on the exit position (the
+        # repeat + next-text directions the successor table writes after timestamp k: cos ~ 0.37 there, <= 0.17
+        # elsewhere) that differ only by +-gamma I_e: A - B writes +-Bx gamma o_I of <|endoftext|>, ending the window
+        # after timestamp k iff L > T_e (12 R of <|endoftext|> against the repeat's 6 R), bounded either way.
+        assert dims.n_dec_layer >= 4, "the variable-length plant needs >= 4 decoder layers"
+        n_ex = len(plan.exits)
+        qx, _ = torch.linalg.qr(torch.cat([V.T.double(), torch.randn(d, n_ex + 1, generator=g, dtype=torch.float64)], 1))
+        Vx = qx.T[V.shape[0]:].float()                  # orthogonal to every planted direction
+        v_ind, v_ball = Vx[:n_ex], Vx[n_ex]
+        lev = sum(LEVEL_W[j] * v_bit[j] for j in range(nb))
+        scale = 35.8 / sq                               # pre-activations in the large-v3 scale for every width
+        o_I, M = 2.0 * R, 20.0 * R
+        p2, p3 = "model.decoder.layers.2.", "model.decoder.layers.3."
+        for pl in (p2, p3):
+            sd[pl + "final_layer_norm.weight"][:] = 1.0
+            sd[pl + "final_layer_norm.bias"][:] = 0.0
+        f1a, b1a, f2a, b2a = (sd[p2 + n] for n in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
+        s_c, K_c = 8.0, 5.0 * scale
+        for e, (k, T) in enumerate(plan.exits):
+            for u, sgn in ((2 * e, 1.0), (2 * e + 1, -1.0)):
+                f1a[u] = s_c * K_c * (lev - T * v_const)
+                b1a[u] = sgn * s_c
+                f2a[:, u] = sgn * (o_I / s_c) * v_ind[e]
+            b2a -= o_I * v_ind[e]
+        b2a += M * v_ball
+        f1b3, b1b3, f2b3, b2b3 = (sd[p3 + n] for n in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
+        beta, gam_x, delta = 10.0 * scale, 5.0 * scale, 40.0
+        th = beta * sq * 7.78 / 21.0 - delta            # B sits DELTA above zero at the exit position
+        Bx = 0.7 * R
+        for e, (k, T) in enumerate(plan.exits):
+            assert plan.kinds[k] == "ts" and len(plan.slots[k]) == 1 and len(plan.slots[k + 1]) == 1
+            u_k = (v_slot[k] + v_slot[k + 1]) / math.sqrt(2.0)
+            ua, ub = 2 * e, 2 * e + 1
+            f1b3[ua] = beta * u_k + gam_x * v_ind[e]
+            f1b3[ub] = beta * u_k
+            b1b3[ua] = -th
+            b1b3[ub] = -th
+            f2b3[:, ua] = Bx * v_eot
+            f2b3[:, ub] = -Bx * v_eot
+        b2b3 -= M * v_ball
+    plan.bit_channels = ([int(c) for c in c_ch] + ([k_ch] if variable else []),
+                         [int(c) for c in c_ref] + ([k_ref] if variable else []))
     return plan
 
 
@@ -437,8 +545,8 @@ def resolve_model(model_size_or_path: str, seed: int = 0, eot_after: Optional[in
         parts = spec.split(":")
         name = parts[1]
         plant = None
-        if parts[-1] == "margin":
-            plant = "margin"
+        if parts[-1] in ("margin", "margin_var"):
+            plant = parts[-1]
             parts = parts[:-1]
         if len(parts) > 2:
             seed = int(parts[2])
