@@ -16,6 +16,7 @@ Prints ONE JSON line on rank 0.  `python bench.py` (N=1) or torch.distributed.ru
 from __future__ import annotations
 
 import argparse
+from typing import Optional
 import json
 import os
 import sys
@@ -46,19 +47,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_shard(rank: int, W: int):
-    """PCM of windows [rank*W, rank*W+W) plus 200-sample margins from the neighbouring clips."""
-    g0 = rank * W
-    clips = [speech_like(30.0, g0 + i) for i in range(W)]
-    left = speech_like(30.0, g0 - 1)[-200:] if g0 > 0 else np.zeros(0, np.float32)
-    right = speech_like(30.0, g0 + W)[:200]
+def build_shard(g0: int, W: int, cache=None):
+    """PCM of windows [g0, g0 + W) of the corpus plus 200-sample margins from the neighbouring clips (window i is
+    speech_like seed i; `cache` maps seeds already generated to their clips)."""
+    cache = {} if cache is None else cache
+
+    def clip(i):
+        if i not in cache:
+            cache[i] = speech_like(30.0, i)
+        return cache[i]
+    clips = [clip(g0 + i) for i in range(W)]
+    left = clip(g0 - 1)[-200:] if g0 > 0 else np.zeros(0, np.float32)
+    right = clip(g0 + W)[:200]
     return np.concatenate([left] + clips + [right]).astype(np.float32), len(left)
 
 
 class Pipeline:
     def __init__(self, eng, tok, dims, rank, world, W, beam, pcm_dev, margin_left, n_total, host_group=None,
-                 words: bool = False, check_every: int = 4):
+                 words: bool = False, check_every: int = 4, g0: Optional[int] = None, max_rows: int = -1):
+        """max_rows: -1 decodes every window in one all-rows batch; >= 0 runs the row-set decode (wm_generate
+        max_rows, 0 = all windows at once) with the windows ordered longest-expected first and compaction."""
         self.eng, self.tok, self.dims = eng, tok, dims
+        self.g0 = rank * W if g0 is None else g0       # first corpus window of this shard
+        self.max_rows = max_rows
         self.check_every = check_every
         self.words = words
         if words:
@@ -85,7 +96,7 @@ class Pipeline:
     def step(self):
         eng, W, d = self.eng, self.W, self.dims
         t0 = time.perf_counter()
-        frame0 = self.rank * W * 3000
+        frame0 = self.g0 * 3000
         mel, gmax = eng.logmel(self.pcm_dev, n_samples=self.n_total, pcm_offset=frame0 * 160 - self.margin_left,
                                frame0=frame0, n_frames=W * 3000)
         if self.world > 1 and self.solo:
@@ -109,12 +120,28 @@ class Pipeline:
         eng.cross_kv(enc, 0)
         torch.cuda.synchronize(eng.device)
         t2 = time.perf_counter()
-        res, steps = eng.generate(list(range(W)), [self.prompt] * W, beam_size=self.beam, suppress_tokens=self.suppress,
-                                  max_length=448, check_every=self.check_every)
+        gen_stats = {}
+        if self.max_rows >= 0 and self.beam == 1:
+            # row-set decode: expected tokens from the shard's frame energy (the VAD stand-in's GPU kernel), windows
+            # started longest-expected first, finished rows refilled / compacted (vlog_amd/shard.py, engine.cpp)
+            from vlog_amd.shard import expected_token_order, expected_tokens
+            db = eng.frame_energy_db(self.pcm_dev, 512)
+            exp = expected_tokens(db, 512, [self.margin_left + CLIP * i for i in range(W)], [CLIP] * W)
+            order = expected_token_order(exp)
+            out, steps = eng.generate(order, [self.prompt] * W, suppress_tokens=self.suppress, max_length=448,
+                                      check_every=self.check_every, max_rows=self.max_rows, compact=True,
+                                      stats=gen_stats)
+            res = [None] * W
+            for w, r in zip(order, out):
+                res[w] = r
+        else:
+            res, steps = eng.generate(list(range(W)), [self.prompt] * W, beam_size=self.beam,
+                                      suppress_tokens=self.suppress, max_length=448, check_every=self.check_every,
+                                      stats=gen_stats)
         t3 = time.perf_counter()
         groups = []
         for w, r in enumerate(res):
-            off = (self.rank * W + w) * 30.0
+            off = (self.g0 + w) * 30.0
             cur, _, _ = split_segments_by_timestamps(r.tokens, d.specials.timestamp_begin, off, 3000, 30.0, w * 3000)
             groups.append(cur)
         t_al = 0.0
@@ -142,7 +169,7 @@ class Pipeline:
         for r in res:
             crc = zlib.crc32(np.asarray(r.tokens, dtype=np.int32).tobytes(), crc)
         self.last = dict(tokens=[len(r.tokens) for r in res], steps=steps, segments=len(segs), vtt_bytes=len(vtt),
-                         crc=crc)
+                         crc=crc, gen_stats=gen_stats)
         if self.keep_windows:
             self.kept = dict(res=res, enc={w: enc[w].float().cpu().numpy() for w in self.keep_windows})
         del enc, mel
@@ -227,7 +254,7 @@ def parity_sample(dims, sd, pipe, fp8_cross: bool = False) -> dict:
     opt = GenerateOptions(suppress_tokens=pipe.suppress, max_length=448)
     ws = sorted(enc)
     g = gate_windows(orc, lambda w: np.stack([enc[i] for i in w]), pipe.prompt, res, dims.specials, opt, pipe.tok,
-                     windows=ws, time_offset=lambda w: (pipe.rank * pipe.W + w) * 30.0)
+                     windows=ws, time_offset=lambda w: (pipe.g0 + w) * 30.0)
     g.pop("oracle_tokens")
     g["windows"] = ws
     g["method"] = ("every sampled window's GPU tokens teacher-forced through oracle/ (bf16-activation mode) on the "
@@ -237,12 +264,13 @@ def parity_sample(dims, sd, pipe, fp8_cross: bool = False) -> dict:
     return g
 
 
-def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
-    """Oracle (numpy fp32, this repo's CPU restatement) on the host cores: one 30 s window's log-mel + encoder,
-    plus `decode_steps` greedy decoder steps, extrapolated to the GPU run's mean tokens per window."""
+def cpu_baseline(dims, sd, mean_tokens: float, n_positions: int = 4):
+    """Oracle (numpy fp32, this repo's CPU restatement) on the host cores: one 30 s window's log-mel + encoder +
+    cross-KV, plus single greedy decoder steps timed at `n_positions` positions spread over the window's mean token
+    count (each after a teacher-forced prefill of the tokens before it, untimed), so the per-step cost covers the
+    growing self-attention; extrapolated to the GPU run's mean tokens per window."""
     sys.path.insert(0, ROOT)
     from oracle import mel as omel
-    from oracle.decode import GenerateOptions, generate_one
     from oracle.model import OracleWhisper
     from vlog_amd.weights import round_bf16
 
@@ -262,11 +290,19 @@ def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
     cross = orc.cross_kv(enc)
     t1 = time.perf_counter()
     prompt = [st.sot, st.lang_token("en"), st.transcribe]
-    r = generate_one(orc, cross, prompt, st, GenerateOptions(max_length=len(prompt) + decode_steps))
-    t2 = time.perf_counter()
-    n_steps = max(1, len(r.tokens))
-    per_step = (t2 - t1) / n_steps
-    per_window = (t1 - t0) + per_step * max(mean_tokens, 1.0)
+    n_tok = max(1, int(round(mean_tokens)))
+    positions = sorted({int(round(i * (n_tok - 1) / max(1, n_positions - 1))) for i in range(n_positions)})
+    rng = np.random.default_rng(0)
+    step_s = []
+    for p in positions:
+        toks = prompt + [int(t) for t in rng.integers(1000, st.eot - 1000, size=p)]      # any text history
+        _, cache = orc.decode(np.asarray([toks]), cross)
+        ts = time.perf_counter()
+        logits, _ = orc.decode(np.asarray([[toks[-1]]]), cross, cache=cache, offset=len(toks))
+        int(np.argmax(logits[0, -1]))                                                    # the greedy pick
+        step_s.append(time.perf_counter() - ts)
+    per_step = float(np.mean(step_s))
+    per_window = (t1 - t0) + per_step * (n_tok + 1)
     threads = share
     if limiter is not None:
         from threadpoolctl import threadpool_info
@@ -277,8 +313,10 @@ def cpu_baseline(dims, sd, mean_tokens: float, decode_steps: int = 12):
             "cpu_model": hc["model"], "host_physical_cores": hc["physical_cores"], "host_logical_cpus": hc["logical_cpus"],
             "process_cpu_share": hc["cpu_share"],
             "sample": (f"oracle/ numpy fp32 CPU restatement, {dims.name}: one 30 s window log-mel+encoder+cross-KV "
-                       f"({t1 - t0:.1f} s) + {n_steps} greedy decoder steps ({per_step:.3f} s/step), extrapolated to "
-                       f"{mean_tokens:.1f} tokens/window; faster-whisper CPU baseline unavailable (not installed)")}
+                       f"({t1 - t0:.1f} s) + greedy decoder steps timed at positions {positions} "
+                       f"({', '.join(f'{1e3 * v:.0f}' for v in step_s)} ms), mean {per_step:.3f} s/step, extrapolated "
+                       f"to {mean_tokens:.1f} tokens + <|endoftext|> per window; faster-whisper CPU baseline "
+                       f"unavailable (not installed)")}
 
 
 def main():
@@ -302,7 +340,20 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-kernel event timing")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity sample (rank 0, untimed)")
     ap.add_argument("--parity-windows", type=int, default=16)
+    ap.add_argument("--workload", choices=("uniform", "variable"), default="uniform",
+                    help="uniform: the margin-planted model (every window ~112 tokens); variable: plant margin_var "
+                         "(a window's audio level sets where its script ends: 1 to ~225 tokens, most 50-150)")
+    ap.add_argument("--max-rows", type=int, default=None,
+                    help="row-set decode with at most this many rows in flight (0 = all windows at once), windows "
+                         "ordered longest-expected first, finished rows refilled / compacted; -1 = one all-rows "
+                         "batch.  Default: -1 for the uniform workload, 0 for the variable one")
+    ap.add_argument("--balance", choices=("count", "tokens"), default=None,
+                    help="N > 1: windows per GPU by count, or by expected tokens (default for --workload variable)")
     args = ap.parse_args()
+    if args.max_rows is None:
+        args.max_rows = 0 if args.workload == "variable" else -1
+    if args.balance is None:
+        args.balance = "tokens" if args.workload == "variable" else "count"
     if args.traffic_json is None:
         args.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r03_c.json")
 
@@ -326,8 +377,9 @@ def main():
 
     dims = model_dims(args.model)
     t = time.perf_counter()
+    plant = "margin_var" if args.workload == "variable" else "margin"
     sd = (synthetic_state_dict(dims, seed=0, eot_after=args.eot_after) if args.random_weights
-          else synthetic_state_dict(dims, seed=0, plant="margin"))
+          else synthetic_state_dict(dims, seed=0, plant=plant))
     from vlog_amd.engine import GpuEngine
     eng = GpuEngine(dims, sd, local)
     if args.cross_fp8:
@@ -339,14 +391,31 @@ def main():
         del sd
         sd = None
     tok = Tokenizer(dims, language="en")
-    W = args.windows
-    pcm, margin = build_shard(rank, W)
+    W_nat = W = args.windows
+    g0 = rank * W
+    cache = {}
+    pcm, margin = build_shard(g0, W, cache)
+    if world > 1 and args.balance == "tokens":
+        # work-balanced shards (vlog_amd/shard.py): every rank estimates the expected tokens of its natural window
+        # range from the GPU frame energy, the estimates are exchanged as host floats, and the corpus is re-cut into
+        # contiguous ranges of equal expected tokens (setup, untimed; a coordinator does the same before dispatch)
+        import torch.distributed as dist
+        from vlog_amd.shard import expected_tokens, partition_by_weight
+        db = eng.frame_energy_db(torch.from_numpy(pcm), 512)
+        est = torch.tensor(expected_tokens(db, 512, [margin + CLIP * i for i in range(W)], [CLIP] * W), dtype=torch.float64)
+        parts = [torch.zeros_like(est) for _ in range(world)]
+        dist.all_gather(parts, est, group=host_group)
+        g0, g1 = partition_by_weight(torch.cat(parts).numpy(), world)[rank]
+        W = g1 - g0
+        pcm, margin = build_shard(g0, W, cache)
+    del cache
     pcm_dev = torch.from_numpy(pcm).to(eng.device)
-    n_total = world * W * CLIP
+    n_total = world * W_nat * CLIP
     eng.reserve(W, W * max(1, args.beam))
-    log(f"[rank {rank}] setup {time.perf_counter() - t:.1f} s, engine {eng.device_bytes() / 2**30:.1f} GiB")
+    log(f"[rank {rank}] setup {time.perf_counter() - t:.1f} s, windows [{g0}, {g0 + W}), engine "
+        f"{eng.device_bytes() / 2**30:.1f} GiB")
     pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total, host_group,
-                    words=args.word_timestamps, check_every=args.check_every)
+                    words=args.word_timestamps, check_every=args.check_every, g0=g0, max_rows=args.max_rows)
 
     def barrier():
         # device drained, then a host-side rendezvous over the gloo group: no RCCL call anywhere in the timed
@@ -384,11 +453,14 @@ def main():
     if dom is not None:
         eng.profile(False)
         prof = eng.profile_read()
+    rank_info = [[elapsed, W, float(sum(pipe.last["tokens"])), pipe.last["steps"]]]
     if world > 1:
         import torch.distributed as dist
-        te = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX, group=host_group)
-        elapsed = float(te.item())
+        te = torch.tensor(rank_info[0], dtype=torch.float64)
+        parts = [torch.zeros_like(te) for _ in range(world)]
+        dist.all_gather(parts, te, group=host_group)
+        rank_info = [p.tolist() for p in parts]
+        elapsed = max(r[0] for r in rank_info)             # the job ends with its slowest rank
     stage_timed = dict(pipe.stage)
     parity = None
     if rank == 0 and not args.no_parity and sd is not None and args.beam == 1:
@@ -400,7 +472,7 @@ def main():
             parity = parity_sample(dims, sd, pipe, fp8_cross=args.cross_fp8)
         except Exception as e:  # reported, never fatal to the GPU measurement
             parity = {"error": str(e)[:300]}
-    audio_s = world * W * 30.0 * args.steps
+    audio_s = world * W_nat * 30.0 * args.steps           # every rank's windows (balanced shards sum to the same)
     value = audio_s / elapsed
     if rank != 0:
         if world > 1:
@@ -421,12 +493,24 @@ def main():
                                f"({'config 5' if args.beam > 1 and args.word_timestamps else 'config 4' if args.beam == 1 else 'beam search'})",
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
+                   "token_length_min_p50_max": [int(np.min(toks)), int(np.median(toks)), int(np.max(toks))],
+                   "decode": ("all-rows batch" if args.max_rows < 0 else
+                              f"row-set (max_rows {args.max_rows or W}, longest-expected first, refill + compaction)"),
+                   "decoder_row_steps": pipe.last["gen_stats"].get("row_steps"),
+                   # live rows / rows in the passes, over the decode (each window's steps incl. its <|endoftext|>)
+                   "active_row_fraction": (round(sum(n + 1 for n in toks) / pipe.last["gen_stats"]["row_steps"], 4)
+                                           if pipe.last["gen_stats"].get("row_steps") else None),
+                   "workload": args.workload,
                    "token_crc32": pipe.last["crc"],
                    "parallelism": f"window-shard x{world}",
                    "weights": (f"synthetic seed 0, random-init + planted eot_after={args.eot_after}" if args.random_weights
-                               else "synthetic seed 0, random-init + margin-planted decoder program (weights.py plant_margin)")},
+                               else f"synthetic seed 0, random-init + margin-planted decoder program (weights.py plant {plant})")},
         "stages_s_per_step": {k: round(v / args.steps, 4) for k, v in stage_timed.items()},
     }
+    if world > 1:
+        out["ranks"] = [{"elapsed_s": round(r[0], 3), "windows": int(r[1]), "tokens": int(r[2]), "decoder_steps": int(r[3])}
+                        for r in rank_info]
+        out["config"]["shard_balance"] = args.balance
     if os.environ.get("VLOG_AMD_BENCH_SHARE_GPU") == "1":
         # a rehearsal of the N > 1 path with several ranks on one device: NOT a scaling result
         out["config"]["gpus_shared"] = True

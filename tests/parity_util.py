@@ -169,8 +169,9 @@ def progress(msg: str) -> None:
 def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists: Sequence[Sequence[int]],
                         ended: Sequence[bool], st, opt: GenerateOptions):
     """Several windows in ONE oracle decoder pass (sequences padded with <|endoftext|>: the mask is causal, so
-    padding never changes an earlier position).  -> per window: (margins [steps], no_speech_prob) with
-    margin = logprob of the GPU token minus the best logprob among the OTHER tokens (> 0: the oracle's argmax)."""
+    padding never changes an earlier position).  -> per window: (margins [steps], no_speech_prob, cum_logprob) with
+    margin = logprob of the GPU token minus the best logprob among the OTHER tokens (> 0: the oracle's argmax) and
+    cum_logprob = the oracle's summed log-prob (after the rules) of the GPU tokens incl. the final <|endoftext|>."""
     cross = orc.cross_kv(enc)
     L = max(len(t) for t in token_lists)
     toks = np.full((len(token_lists), len(prompt) + L), st.eot, dtype=np.int64)
@@ -183,10 +184,12 @@ def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists
     for i, t in enumerate(token_lists):
         seq = list(t) + ([st.eot] if ended[i] else [])
         ms = np.empty(len(seq))
+        cum = 0.0
         for k, tok in enumerate(seq):
             # the margin of the rule-masked logits equals that of their log-softmax (same shift)
             x = apply_rules(logits[i, P - 1 + k], list(t[:k]), st, opt.suppress_tokens, opt.suppress_blank,
                             opt.max_initial_timestamp_index, opt.with_timestamps)
+            cum += float(log_softmax(x)[tok])
             chosen = x[tok]
             x[tok] = -np.inf
             ms[k] = chosen - np.max(x) if np.isfinite(chosen) else -np.inf
@@ -194,7 +197,7 @@ def teacher_force_batch(orc, enc: np.ndarray, prompt: Sequence[int], token_lists
         ns = 0.0
         if st.sot in prompt:
             ns = float(np.exp(log_softmax(logits[i, list(prompt).index(st.sot)]))[st.no_speech])
-        out.append((ms, ns))
+        out.append((ms, ns, cum))
     return out
 
 
@@ -281,6 +284,7 @@ def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateO
     import time
     ws = list(range(len(results))) if windows is None else list(windows)
     ident, margins, ns_diff, non_ident = [], [], 0.0, []
+    cum_diff = 0.0                      # worst |GPU cum_logprob - oracle teacher-forced sum| (relative to max(1, |sum|))
     oracle_tokens = {}
     t0 = time.time()
     todo = []
@@ -296,10 +300,13 @@ def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateO
         enc = enc_of(cw)
         toks = [list(results[w].tokens) for w in cw]
         ended = [len(prompt) + len(t) < opt.max_length for t in toks]
-        for j, (w, (ms, ns)) in enumerate(zip(cw, teacher_force_batch(orc, enc, prompt, toks, ended, st, opt))):
+        for j, (w, (ms, ns, cum)) in enumerate(zip(cw, teacher_force_batch(orc, enc, prompt, toks, ended, st, opt))):
             same = bool(np.all(ms > 0.0))
             ident.append(same)
             ns_diff = max(ns_diff, abs(ns - float(results[w].no_speech_prob)))
+            cg = getattr(results[w], "cum_logprob", None)
+            if cg is not None and np.isfinite(cum):
+                cum_diff = max(cum_diff, abs(float(cg) - cum) / max(1.0, abs(cum)))
             if same:
                 oracle_tokens[w] = toks[j]
                 margins.append(float(np.min(ms)) if ms.size else 0.0)
@@ -324,14 +331,21 @@ def gate_windows(orc, enc_of, prompt: Sequence[int], results, st, opt: GenerateO
     return {"n": n, "identical": int(sum(ident)), "identical_frac": round(sum(ident) / max(n, 1), 5),
             "wer_delta": round(errs / max(n_ref, 1), 6), "segment_max_dt_s": round(dt, 4),
             "segment_count_mismatch": seg_mismatch, "max_no_speech_diff": ns_diff,
+            "max_cum_logprob_rel_diff": cum_diff,
             "min_margin_identical_nats": round(min(margins), 3) if margins else None,
             "non_identical_windows": non_ident, "oracle_passes": len(todo),
             "oracle_tokens": oracle_tokens,
             "gates": {"identical_frac": GATE_IDENTICAL, "wer_delta": GATE_WER, "segment_dt_s": GATE_DT}}
 
 
+GATE_CUM_REL = 2e-2        # the GPU's cumulative log-prob vs the oracle's teacher-forced sum (relative to max(1, |sum|))
+GATE_NO_SPEECH = 1e-3      # no-speech probability
+
+
 def assert_gates(g: dict) -> None:
     assert g["identical_frac"] >= GATE_IDENTICAL, g
+    assert g["max_cum_logprob_rel_diff"] <= GATE_CUM_REL, g
+    assert g["max_no_speech_diff"] <= GATE_NO_SPEECH, g
     assert g["wer_delta"] <= GATE_WER, g
     assert g["segment_max_dt_s"] <= GATE_DT + 1e-9, g
     assert g["segment_count_mismatch"] <= (1.0 - GATE_IDENTICAL) * g["n"], g

@@ -37,16 +37,17 @@ def _record(name, g):
 
 
 class MarginConfig:
-    def __init__(self, name, n_windows, seed0=0):
+    def __init__(self, name, n_windows, seed0=0, plant="margin"):
         from vlog_amd.engine import GpuEngine
         self.dims = dims = model_dims(name)
-        sd = synthetic_state_dict(dims, seed=0, plant="margin")
+        sd = synthetic_state_dict(dims, seed=0, plant=plant)
         self.eng = GpuEngine(dims, sd, 0)
         self.w = round_bf16(sd)
         del sd
         self.orc = OracleWhisper(self.w, dims, np.float32, bf16_acts=True)
         self.W = n_windows
         x = np.concatenate([speech_like(30.0, seed0 + i) for i in range(n_windows)])
+        self.audio = x
         self.mel = self.eng.features(torch.from_numpy(x))
         self.enc = self.eng.encode(self.mel, [3000 * i for i in range(n_windows)], [3000] * n_windows)
         self.tok = Tokenizer(dims, language="en")
@@ -60,12 +61,17 @@ class MarginConfig:
     def enc_of(self, ws):
         return self.enc[list(ws)].float().cpu().numpy()
 
-    def greedy(self):
+    def greedy(self, order=None, **kw):
+        """Greedy decode of every window (slots in `order`, default 0..W-1); results by window."""
+        order = list(range(self.W)) if order is None else list(order)
         self.eng.reserve(self.W, self.W)
         self.eng.cross_kv(self.enc, 0)
-        res, _ = self.eng.generate(list(range(self.W)), [self.prompt] * self.W, suppress_tokens=self.sup,
-                                   max_length=448, check_every=4)
-        return res
+        res, self.steps = self.eng.generate(order, [self.prompt] * self.W, suppress_tokens=self.sup, max_length=448,
+                                            check_every=4, **kw)
+        out = [None] * self.W
+        for w, r in zip(order, res):
+            out[w] = r
+        return out
 
     def gates(self, name, res, known=None):
         g = gate_windows(self.orc, self.enc_of, self.prompt, res, self.st, self.opt(), self.tok, known=known)
@@ -205,3 +211,39 @@ def test_config1_tiny_en_vtt_identical_to_cpu_oracle(tmp_path):
     _record("gates tiny.en 60 s VTT vs CPU oracle", dict(vtt_identical=vtt == vtt_ref, wer=wer, cues=vtt.count(" --> ")))
     assert vtt == vtt_ref
     assert wer == 0.0 and vtt.count(" --> ") >= 8
+
+
+# ------------------------------------------------------------------------------------------ variable-length workload
+@pytest.fixture(scope="module")
+def lv3_var():
+    return MarginConfig("large-v3", 150, plant="margin_var")
+
+
+def test_config4_variable_length_gates_and_row_set_decode(lv3_var):
+    """Config 4 on the variable-length planted model (weights.py plant margin_var: the window's audio level picks
+    where its script ends — one token to ~225, most 50-150): every window gated against the oracle, with the
+    all-rows decode and with the row-set decode the bench runs (windows ordered longest-expected first by
+    vlog_amd.shard.expected_tokens, rows refilled as windows end, then compacted), whose tokens must equal the
+    all-rows decode's on every window (the model is decisive; the routes differ only in f32 rounding)."""
+    from vlog_amd.shard import expected_token_order, expected_tokens
+    cfg = lv3_var
+    res = cfg.greedy()
+    steps_all = cfg.steps
+    g = cfg.gates("gates large-v3 variable-length greedy 150 windows", res)
+    assert_gates(g)
+    lens = [len(r.tokens) for r in res]
+    assert min(lens) <= 5 and max(lens) >= 170 and 60 <= float(np.mean(lens)) <= 160, lens
+    db = cfg.eng.frame_energy_db(torch.from_numpy(cfg.audio), 512)
+    expect = expected_tokens(db, 512, [480000 * i for i in range(cfg.W)], [480000] * cfg.W)
+    order = expected_token_order(expect)
+    corr = float(np.corrcoef(expect, lens)[0, 1])
+    st = {}
+    rows = cfg.greedy(order=order, max_rows=112, compact=True, stats=st)
+    same = sum(a.tokens == b.tokens for a, b in zip(res, rows))
+    _record("row-set decode large-v3 variable-length 150 windows", dict(
+        same_tokens=same, stats=st, steps_all_rows=steps_all, mean_tokens=float(np.mean(lens)),
+        expected_vs_actual_tokens_corr=corr,
+        lengths_min_max=(min(lens), max(lens)),
+        active_row_fraction_all_rows=float(sum(n + 1 for n in lens) / (steps_all * cfg.W)),
+        active_row_fraction_row_set=float(sum(n + 1 for n in lens) / max(1, st["row_steps"]))))
+    assert same == cfg.W, same

@@ -1575,7 +1575,14 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
     if (nt[i] <= 0 || S[i] > m.n_text_ctx) throw std::runtime_error("wm_align_batch: bad token count");
     if (F[i] <= 0 || F[i] > T) throw std::runtime_error("wm_align_batch: bad num_frames");
   }
-  const double budget = 1.5e9;
+  // The capture buffer (S x heads x 1500 f32 per item: ~230 MB for a large-v3 window with the default 320 heads)
+  // may take half of the free device memory (at most 48 GB): a batch of 150 large-v3 windows then aligns in ONE
+  // teacher-forced pass instead of ~25 passes of 6 windows under a fixed 1.5 GB budget (round 3: 0.89 s per
+  // 150-window step, most of it those passes).
+  size_t free_b = 0, total_b = 0;
+  HIP_OK(hipMemGetInfo(&free_b, &total_b));
+  const double reusable = (double)e->a_attn.bytes + (double)e->a_logits.bytes;
+  const double budget = std::max(1.5e9, std::min(48e9, 0.5 * (double)free_b + reusable));
   int i0 = 0;
   while (i0 < n) {
     int i1 = i0, smax = 0;

@@ -43,6 +43,68 @@ def partition_windows(n_windows: int, world: int) -> List[Tuple[int, int]]:
     return out
 
 
+# ----------------------------------------------------------------------------------- expected work per window
+# A window's decode cost follows its token count (the decoder steps), which follows how much of it is speech.
+# The estimate below is the scheduler's only view of it: speech seconds from the per-frame log energy the VAD
+# stand-in already computes on the GPU (wm_frame_energy), within 40 dB of the file's loud frames, times a
+# speaking rate.  Only its order and relative size matter: the row-set decode starts the longest-expected
+# windows first (so the short ones fill in behind them: longest-processing-time-first), and the shard partition
+# balances the expected tokens per GPU instead of the window count.
+TOKENS_PER_SPEECH_SECOND = 4.0
+
+
+def speech_frames(frame_db: np.ndarray) -> np.ndarray:
+    """Frames within 40 dB of the file's loud frames (its 99th-percentile frame) and above -70 dBFS."""
+    db = np.asarray(frame_db, dtype=np.float64)
+    finite = db[db > -100.0]
+    peak = float(np.percentile(finite, 99)) if finite.size else -100.0
+    return db > max(peak - 40.0, -70.0)
+
+
+def expected_tokens(frame_db: np.ndarray, frame: int, starts: Sequence[int], lengths: Sequence[int]) -> np.ndarray:
+    """Expected tokens of each window [starts[i], starts[i] + lengths[i]) (samples) from per-frame dB of `frame`
+    samples: speech seconds x TOKENS_PER_SPEECH_SECOND, at least 1."""
+    sp = speech_frames(frame_db).astype(np.int64)
+    csum = np.concatenate([[0], np.cumsum(sp)])
+    out = np.empty(len(starts), dtype=np.float64)
+    for i, (s, n) in enumerate(zip(starts, lengths)):
+        a = min(len(sp), s // frame)
+        b = min(len(sp), max(a, -(-(s + n) // frame)))
+        out[i] = max(1.0, (csum[b] - csum[a]) * frame / SAMPLE_RATE * TOKENS_PER_SPEECH_SECOND)
+    return out
+
+
+def expected_token_order(tokens: Sequence[float]) -> List[int]:
+    """Window indices longest-expected first (stable)."""
+    return [int(i) for i in np.argsort(-np.asarray(tokens, dtype=np.float64), kind="stable")]
+
+
+def partition_by_weight(weights: Sequence[float], world: int) -> List[Tuple[int, int]]:
+    """Contiguous [start, end) window ranges, one per rank, with the summed weights (expected tokens) as equal as
+    contiguity allows: rank r ends where the running sum first reaches (r + 1) / world of the total, at the nearer
+    window boundary; every rank keeps at least one window while windows remain."""
+    w = np.asarray(weights, dtype=np.float64)
+    n = w.size
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    csum = np.concatenate([[0.0], np.cumsum(w)])
+    total = csum[-1]
+    out, s = [], 0
+    for r in range(world):
+        if r == world - 1:
+            e = n
+        else:
+            target = total * (r + 1) / world
+            e = int(np.searchsorted(csum, target))              # csum[e] >= target
+            if e > 0 and target - csum[e - 1] < csum[min(e, n)] - target:
+                e -= 1
+            e = max(e, s + 1 if s < n else s)                   # at least one window
+            e = min(e, n - max(0, min(world - 1 - r, n - s - 1)))   # and one for each later rank, while they last
+        out.append((s, e))
+        s = e
+    return out
+
+
 @dataclass
 class ShardPlan:
     rank: int
@@ -56,11 +118,16 @@ class ShardPlan:
     offsets: List[float]             # absolute window start times (s)
 
 
-def plan_shards(n_samples: int, world: int) -> List[ShardPlan]:
+def plan_shards(n_samples: int, world: int, weights: Optional[Sequence[float]] = None) -> List[ShardPlan]:
+    """Per-rank plans; `weights` (expected tokens per window, expected_tokens) balances the work instead of the
+    window count."""
     cf = content_frames(n_samples)
     n_win = max(1, -(-cf // N_FRAMES))
     plans = []
-    for rank, (w0, w1) in enumerate(partition_windows(n_win, world)):
+    parts = partition_by_weight(weights, world) if weights is not None else partition_windows(n_win, world)
+    if weights is not None and len(weights) != n_win:
+        raise ValueError(f"plan_shards: {len(weights)} weights for {n_win} windows")
+    for rank, (w0, w1) in enumerate(parts):
         f0 = min(w0 * N_FRAMES, (cf + 1) & ~1)   # even: the log-mel kernel transforms (even, odd) frame pairs
         f1 = min(cf, w1 * N_FRAMES)
         if w1 == n_win and w1 > w0:
