@@ -37,8 +37,8 @@ from vlog_amd.weights import round_bf16, synthetic_state_dict
 pytestmark = pytest.mark.gpu
 
 BAR = 0.02          # nats, bf16 engine vs bf16-format oracle, every step
-FP8_BAR = 1.0       # nats, fp8 cross memory vs the full-precision oracle, every step (max)
-FP8_P99 = 0.25      # nats, its 99th percentile over all steps
+FP8_BAR = 0.05      # nats, fp8 cross memory vs the full-precision oracle, every step (max; measured 0.014)
+FP8_P99 = 0.02      # nats, its 99th percentile over all steps (measured 0.0087)
 
 
 def _record(name, **kw):
@@ -88,6 +88,7 @@ def sweep(cfg: RandomConfig, runs, chunk=8):
     dev = {n: [] for n in names}
     ties = {n: 0 for n in names}
     worst = {n: (0.0, -1, -1) for n in names}
+    margin = {n: 0.0 for n in names}
     for c0 in range(0, W, chunk):
         progress(f"logprob sweep {cfg.dims.name}: windows {c0}/{W}")
         ws = list(range(c0, min(W, c0 + chunk)))
@@ -104,6 +105,10 @@ def sweep(cfg: RandomConfig, runs, chunk=8):
                 continue
             d, t = record_deviation(r.token_logprobs, rec)
             dev[n].append(d)
+            # the oracle's margin of the GPU's token over the best other (tie-aware as record_deviation): a greedy
+            # decode must have picked the oracle's best to within the noise bar
+            tie = (np.abs(rec[:, 2]) <= 0.05) & (np.abs(np.asarray(r.token_logprobs) - rec[:, 1]) < d + 1e-12)
+            margin[n] = min(margin[n], float(np.min(np.where(tie, 0.0, rec[:, 0] - rec[:, 3]))) if len(rec) else 0.0)
             ties[n] += t
             k = int(np.argmax(d)) if d.size else -1
             if d.size and d[k] > worst[n][0]:
@@ -114,7 +119,8 @@ def sweep(cfg: RandomConfig, runs, chunk=8):
         a = np.concatenate(dev[n]) if dev[n] else np.zeros(0)
         out[n] = dict(steps=int(a.size), max=float(a.max()) if a.size else 0.0,
                       p99=float(np.percentile(a, 99)) if a.size else 0.0, mean=float(a.mean()) if a.size else 0.0,
-                      over_bar=int((a > BAR).sum()), rule_tie_steps=ties[n], worst=worst[n])
+                      over_bar=int((a > BAR).sum()), rule_tie_steps=ties[n], worst=worst[n],
+                      min_oracle_margin=margin[n])
     return out
 
 
@@ -131,7 +137,7 @@ def _greedy_case(name, W):
     _self_consistent(res)
     s = sweep(cfg, {"greedy": res})["greedy"]
     _record(f"logprob records {name} greedy {W} windows", bar=BAR, **s)
-    assert s["max"] <= BAR, s
+    assert s["max"] <= BAR and s["min_oracle_margin"] >= -BAR, s
     return cfg, res
 
 
@@ -158,7 +164,9 @@ def test_row_set_decode_every_step():
     _record("logprob records base greedy 32 windows, row-set decode (12 rows, compact)", bar=BAR, same_tokens=same,
             stats=st, **s)
     assert s["max"] <= BAR, s
-    assert same >= 28, same
+    # the random model's near-ties part the two decodes on some windows (22/32 identical measured); every token of
+    # the row-set decode is the oracle's greedy choice to within the bar
+    assert s["min_oracle_margin"] >= -BAR, s
 
 
 @pytest.fixture(scope="module")
@@ -189,6 +197,6 @@ def test_config4_5_large_v3_greedy_beam_fp8_every_step(lv3):
     same_fp8 = sum(a.tokens == b.tokens for a, b in zip(greedy, fp8))
     _record("logprob records large-v3: greedy 150 / fp8 150 (vs full-precision oracle) / beam5 128",
             bar=BAR, fp8_bar=FP8_BAR, fp8_p99_bar=FP8_P99, fp8_windows_identical_to_bf16=same_fp8, **s)
-    assert s["greedy"]["max"] <= BAR, s["greedy"]
+    assert s["greedy"]["max"] <= BAR and s["greedy"]["min_oracle_margin"] >= -BAR, s["greedy"]
     assert s["beam5"]["max"] <= BAR, s["beam5"]
     assert s["fp8"]["max"] <= FP8_BAR and s["fp8"]["p99"] <= FP8_P99, s["fp8"]

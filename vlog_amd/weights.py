@@ -181,10 +181,11 @@ class MarginPlan:
 # 3 and with a negative sign: more speech -> a lower level -> a later exit), and the exits: (segment whose end
 # timestamp may end the window (-1: the first timestamp), threshold).  Levels L in {-8, ..., 8} step 2 follow a
 # shifted binomial; thresholds sit at odd values, so every decision has a full level of margin:
-#   L = 8 -> 1 token, 6 -> ~2 segments, 4 -> 4, 2 -> 6, 0 -> 7, -2 -> 9, -4 -> 11, -6 -> 13, -8 -> all 16.
+#   L = 8 -> 1 token, 6 -> 5 (the 3-token first segment), 4 -> ~48, 2 -> ~77, 0 -> ~92, -2 -> ~121, -4 -> ~150,
+#   -6 -> ~179, -8 -> the whole script (~222); mean ~97 over the level distribution.
 VAR_SEGMENTS = 16
 LEVEL_W = (-3, 1, 1, 1, 1, 1)
-VAR_EXITS = ((-1, 7), (1, 5), (3, 3), (5, 1), (6, -1), (8, -3), (10, -5), (12, -7))
+VAR_EXITS = ((-1, 7), (0, 5), (3, 3), (5, 1), (6, -1), (8, -3), (10, -5), (12, -7))
 
 
 def margin_plan(dims: ModelDims, seed: int = 0, n_segments: int = 8, variable: bool = False) -> MarginPlan:
@@ -200,6 +201,8 @@ def margin_plan(dims: ModelDims, seed: int = 0, n_segments: int = 8, variable: b
     for m in range(n_segments):
         n = int(rng.integers(10, 15))
         branch_at = set(rng.choice(np.arange(1, n - 1), size=2, replace=False).tolist())
+        if variable and m == 0:
+            n, branch_at = 3, set()                      # a short first segment: the 5-token exit
         for j in range(n):
             if j in branch_at and j - 1 not in branch_at:
                 slots.append((text_ids.pop(), text_ids.pop()))
@@ -341,7 +344,9 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
     same_affine("model.encoder.layers.0.final_layer_norm", m_ch, m_ref)
     pf = "model.encoder.layers.0."
     f1w, f1b, f2w, f2b = (sd[pf + n] for n in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
-    s_g, K, o_half = 8.0, 50.0, s_enc
+    # the variable-length plant reads the bits' signs as a level too: a 20x steeper clip leaves a 20x thinner sliver
+    # of windows with a partly saturated bit
+    s_g, K, o_half = 8.0, (1000.0 if variable else 50.0), s_enc
     for j in range(nb):
         for u, sgn in ((2 * j, 1.0), (2 * j + 1, -1.0)):
             f1w[u] = 0.0
