@@ -174,6 +174,77 @@ class Pipeline:
             self.kept = dict(res=res, enc={w: enc[w].float().cpu().numpy() for w in self.keep_windows})
         del enc, mel
 
+    def run_stream(self, K: int):
+        """K batches of this shard's W windows through ONE continuous row-set decode: every batch's log-mel +
+        encoder output goes to its own window slots (K x W slots), then the windows of all K batches decode with W
+        rows in flight, longest-expected first, a finished window's row taking the next window (engine.cpp
+        generate_rows) — so a batch's short windows no longer wait for its longest one: the decoder steps follow the
+        total tokens, plus one tail at the end.  A production worker streaming its shard does the same.  Results,
+        segments and the WebVTT are produced for every window of every batch."""
+        from vlog_amd.shard import expected_token_order, expected_tokens
+        eng, W, d = self.eng, self.W, self.dims
+        t0 = time.perf_counter()
+        frame0 = self.g0 * 3000
+        t_mel = t_enc = 0.0
+        for k in range(K):
+            ta = time.perf_counter()
+            mel, gmax = eng.logmel(self.pcm_dev, n_samples=self.n_total, pcm_offset=frame0 * 160 - self.margin_left,
+                                   frame0=frame0, n_frames=W * 3000)
+            if self.world > 1:
+                import torch.distributed as dist
+                g = torch.tensor([eng.gmax_value(gmax)], dtype=torch.float32)
+                dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.host_group)
+                self.last_gmax = float(g[0])
+                eng.logmel_finalize(mel, gmax, self.last_gmax)
+            else:
+                eng.logmel_finalize(mel, gmax)
+            tb = time.perf_counter()
+            enc = eng.encode(mel, [i * 3000 for i in range(W)], [3000] * W)
+            eng.cross_kv(enc, k * W)
+            del enc, mel
+            torch.cuda.synchronize(eng.device)
+            tc = time.perf_counter()
+            t_mel += tb - ta
+            t_enc += tc - tb
+        t2 = time.perf_counter()
+        db = eng.frame_energy_db(self.pcm_dev, 512)
+        exp = expected_tokens(db, 512, [self.margin_left + CLIP * i for i in range(W)], [CLIP] * W)
+        order = expected_token_order(np.tile(exp, K))
+        gen_stats = {}
+        out, steps = eng.generate(order, [self.prompt] * (K * W), suppress_tokens=self.suppress, max_length=448,
+                                  check_every=self.check_every, max_rows=W, compact=True, stats=gen_stats)
+        res = [None] * (K * W)
+        for w, r in zip(order, out):
+            res[w] = r
+        t3 = time.perf_counter()
+        n_seg = vtt_bytes = 0
+        for k in range(K):
+            segs = []
+            for w in range(W):
+                off = (self.g0 + w) * 30.0
+                cur, _, _ = split_segments_by_timestamps(res[k * W + w].tokens, d.specials.timestamp_begin, off, 3000,
+                                                         30.0, w * 3000)
+                for s_ in cur:
+                    text = self.tok.decode(s_["tokens"])
+                    if s_["start"] == s_["end"] or not text.strip():
+                        continue
+                    segs.append({"start": s_["start"], "end": s_["end"], "text": text})
+            vtt = generate_webvtt(segs)
+            n_seg += len(segs)
+            vtt_bytes += len(vtt)
+        t4 = time.perf_counter()
+        for k_, v in (("logmel", t_mel), ("encode", t_enc), ("schedule", 0.0), ("decode", t3 - t2), ("align", 0.0),
+                      ("host", t4 - t3)):
+            self.stage[k_] = self.stage.get(k_, 0.0) + v
+        import zlib
+        crc = 0
+        for r in res[:W]:
+            crc = zlib.crc32(np.asarray(r.tokens, dtype=np.int32).tobytes(), crc)
+        self.last = dict(tokens=[len(r.tokens) for r in res[:W]], steps=steps / K, segments=n_seg, vtt_bytes=vtt_bytes,
+                         crc=crc, gen_stats=gen_stats, stream_batches=K,
+                         all_tokens=[len(r.tokens) for r in res])
+        return time.perf_counter() - t0
+
 
 def host_cpu() -> dict:
     """lscpu model name and physical core count of this host (the CPU baseline states both)."""
@@ -347,6 +418,9 @@ def main():
                     help="row-set decode with at most this many rows in flight (0 = all windows at once), windows "
                          "ordered longest-expected first, finished rows refilled / compacted; -1 = one all-rows "
                          "batch.  Default: -1 for the uniform workload, 0 for the variable one")
+    ap.add_argument("--stream", action="store_true",
+                    help="the --steps batches of the shard through ONE continuous row-set decode (Pipeline.run_stream): "
+                         "finished windows' rows refilled from the next batch; ms_per_step = total / steps")
     ap.add_argument("--balance", choices=("count", "tokens"), default=None,
                     help="N > 1: windows per GPU by count, or by expected tokens (default for --workload variable)")
     args = ap.parse_args()
@@ -411,7 +485,7 @@ def main():
     del cache
     pcm_dev = torch.from_numpy(pcm).to(eng.device)
     n_total = world * W_nat * CLIP
-    eng.reserve(W, W * max(1, args.beam))
+    eng.reserve(W * (args.steps if args.stream else 1), W * max(1, args.beam))
     log(f"[rank {rank}] setup {time.perf_counter() - t:.1f} s, windows [{g0}, {g0 + W}), engine "
         f"{eng.device_bytes() / 2**30:.1f} GiB")
     pipe = Pipeline(eng, tok, dims, rank, world, W, args.beam, pcm_dev, margin, n_total, host_group,
@@ -445,15 +519,18 @@ def main():
     if dom is not None:                       # timed region: events on the dominant class only
         eng.profile(True, classes=[dom])
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.step()
+    if args.stream:
+        pipe.run_stream(args.steps)
+    else:
+        for _ in range(args.steps):
+            pipe.step()
     barrier()
     elapsed = time.perf_counter() - t0
     prof = None
     if dom is not None:
         eng.profile(False)
         prof = eng.profile_read()
-    rank_info = [[elapsed, W, float(sum(pipe.last["tokens"])), pipe.last["steps"]]]
+    rank_info = [[elapsed, W, float(sum(pipe.last.get("all_tokens", pipe.last["tokens"]))), pipe.last["steps"]]]
     if world > 1:
         import torch.distributed as dist
         te = torch.tensor(rank_info[0], dtype=torch.float64)
@@ -494,11 +571,14 @@ def main():
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
                    "token_length_min_p50_max": [int(np.min(toks)), int(np.median(toks)), int(np.max(toks))],
-                   "decode": ("all-rows batch" if args.max_rows < 0 else
+                   "decode": (f"continuous row-set over the {args.steps} batches ({W} rows, longest-expected first, "
+                              f"refill across batches + compaction)" if args.stream else
+                              "all-rows batch" if args.max_rows < 0 else
                               f"row-set (max_rows {args.max_rows or W}, longest-expected first, refill + compaction)"),
                    "decoder_row_steps": pipe.last["gen_stats"].get("row_steps"),
                    # live rows / rows in the passes, over the decode (each window's steps incl. its <|endoftext|>)
-                   "active_row_fraction": (round(sum(n + 1 for n in toks) / pipe.last["gen_stats"]["row_steps"], 4)
+                   "active_row_fraction": (round(sum(n + 1 for n in pipe.last.get("all_tokens", toks))
+                                                 / pipe.last["gen_stats"]["row_steps"], 4)
                                            if pipe.last["gen_stats"].get("row_steps") else None),
                    "workload": args.workload,
                    "token_crc32": pipe.last["crc"],

@@ -93,8 +93,9 @@ def tiny_var():
 def test_variable_length_follows_the_window_level(tiny_var):
     """The script ends after the first exit timestamp whose threshold the window's level exceeds: lengths from
     1 token to the whole script, each an exact prefix of the planted script (+ its timestamp pairs)."""
-    from vlog_amd.weights import LEVEL_W
+    from vlog_amd.weights import level_weights
     dims, plan, _, enc, _, _, _, res = tiny_var
+    LEVEL_W = level_weights(dims.n_mels)
     c, cr = plan.bit_channels
     lengths = []
     for i, r in enumerate(res):

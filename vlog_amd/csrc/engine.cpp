@@ -1012,7 +1012,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   };
   select(0);
   int steps = 1;
-  long long row_steps = 0;
+  long long row_steps = NH;                      // the prefill pass selects every hypothesis' first token
   int captures = 0;
   const int max_steps = a->max_length - P;      // generated tokens (incl. the final one) <= max_length - P
   const int check = std::max(1, a->check_every);

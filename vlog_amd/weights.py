@@ -185,6 +185,14 @@ class MarginPlan:
 #   -6 -> ~179, -8 -> the whole script (~222); mean ~97 over the level distribution.
 VAR_SEGMENTS = 16
 LEVEL_W = (-3, 1, 1, 1, 1, 1)
+
+
+def level_weights(n_mels: int) -> Tuple[int, ...]:
+    """LEVEL_W with bit 0's sign oriented so that MORE speech lowers the level (a later exit): the first principal
+    component's sign is arbitrary per calibration table (n_mels 80: it grows with the window's energy, 128: it
+    falls), so the weight follows the sign of its loadings."""
+    p0 = float(np.sum(np.asarray(_margin_calib(n_mels)["proj"])[:, 0]))
+    return (LEVEL_W[0] * (1 if p0 >= 0 else -1),) + tuple(LEVEL_W[1:])
 VAR_EXITS = ((-1, 7), (0, 5), (3, 3), (5, 1), (6, -1), (8, -3), (10, -5), (12, -7))
 
 
@@ -458,7 +466,8 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
         qx, _ = torch.linalg.qr(torch.cat([V.T.double(), torch.randn(d, n_ex + 1, generator=g, dtype=torch.float64)], 1))
         Vx = qx.T[V.shape[0]:].float()                  # orthogonal to every planted direction
         v_ind, v_ball = Vx[:n_ex], Vx[n_ex]
-        lev = sum(LEVEL_W[j] * v_bit[j] for j in range(nb))
+        lw = level_weights(dims.n_mels)
+        lev = sum(lw[j] * v_bit[j] for j in range(nb))
         scale = 35.8 / sq                               # pre-activations in the large-v3 scale for every width
         o_I, M = 2.0 * R, 20.0 * R
         p2, p3 = "model.decoder.layers.2.", "model.decoder.layers.3."
