@@ -303,12 +303,23 @@ static int ring_pk() {
   return v;
 }
 
-template <int MF, int KIND, int NC>
-static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     int splitk, int kr, hipStream_t st) {
+// LDS budget of a ring block: 144 KiB (one block per CU: the deepest ring) or 72 KiB (VLOG_AMD_RING_LDS=72: two
+// resident blocks per CU, twice the DMA requests in flight per CU with half the ring depth each).
+static int ring_lds_kb() {
+  static const int v = [] {
+    const char* e = std::getenv("VLOG_AMD_RING_LDS");
+    return e && std::atoi(e) == 72 ? 72 : 144;
+  }();
+  return v;
+}
+
+template <int MF, int KIND, int NC, int CAPKB>
+static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                         int splitk, int kr, hipStream_t st) {
   constexpr int SUBB = (MF * 16 + 32 * NC) * 128;      // bytes of one 64-k sub-panel
-  constexpr int R = NC == 1 ? (MF <= 4 ? 8 : MF <= 8 ? 7 : 6) : std::min(8, (144 * 1024) / SUBB);   // <= 144 KiB
-  constexpr int R2 = std::min(8, (144 * 1024) / (2 * SUBB)), R4 = std::min(8, (144 * 1024) / (4 * SUBB));
+  constexpr int CAP = CAPKB * 1024;
+  constexpr int R = std::max(2, NC == 1 ? std::min(MF <= 4 ? 8 : MF <= 8 ? 7 : 6, CAP / SUBB) : std::min(8, CAP / SUBB));
+  constexpr int R2 = std::min(8, CAP / (2 * SUBB)), R4 = std::min(8, CAP / (4 * SUBB));
   const int tiles_n = (N + 32 * NC - 1) / (32 * NC);
   const int rgroups = (M + MF * 16 - 1) / (MF * 16);
   const dim3 grid(tiles_n * rgroups * splitk);
@@ -329,9 +340,17 @@ static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
       return;
     }
   }
+  static_assert(R * SUBB <= 160 * 1024, "ring exceeds the LDS");
   hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R, 1, NC>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk,
                      kr, ws, rgroups);
   WM_LAUNCH_CHECK("dec_ring_kernel");
+}
+
+template <int MF, int KIND, int NC>
+static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                     int splitk, int kr, hipStream_t st) {
+  if (ring_lds_kb() == 72) run_ring_cap<MF, KIND, NC, 72>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_ring_cap<MF, KIND, NC, 144>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
 // rows_per_block 0: one row group covering every row (MF from M); else 32 / 64 / 96 / 128 / 160 rows per block
