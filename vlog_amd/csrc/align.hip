@@ -63,33 +63,45 @@ __global__ void align_rowsum_kernel(const float* __restrict__ attn, int S, int n
 }
 
 #define MEDW_MAX 15
-__global__ void align_median_kernel(const float* __restrict__ z, int S, int nh, int F, int width, int r0, int nrows,
-                                    float* __restrict__ mat) {
+// Per (output row, frame): the width-W median along time of every head's z row (reflect padding, as
+// transformers' _median_filter), averaged over the heads and negated.  The median is an odd-even transposition
+// sort of the W values in registers (W rounds of compare-exchanges with compile-time indices: no scratch, no
+// divergent branches; the earlier insertion sort indexed a private array dynamically, which the compiler spills to
+// scratch) — an exact selection, so the result is unchanged.
+template <int WIDTH>
+__global__ __launch_bounds__(128) void align_median_kernel(const float* __restrict__ z, int S, int nh, int F, int r0,
+                                                           int nrows, float* __restrict__ mat) {
   const int r = blockIdx.y;          // output row: token row r0 + r
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F || r >= nrows) return;
-  const int pad = width / 2;
+  constexpr int PAD = WIDTH / 2;
+  int idx[WIDTH];
+#pragma unroll
+  for (int k = 0; k < WIDTH; ++k) {
+    int i = f - PAD + k;
+    if (i < 0) i = -i;
+    if (i >= F) i = 2 * (F - 1) - i;
+    idx[k] = min(max(i, 0), F - 1);
+  }
   float acc = 0.f;
   for (int h = 0; h < nh; ++h) {
     const float* row = z + ((long long)h * S + r0 + r) * F;
     float v;
-    if (F <= pad) {
+    if (F <= PAD) {
       v = row[f];
     } else {
-      float win[MEDW_MAX];
-      for (int k = 0; k < width; ++k) {
-        int idx = f - pad + k;
-        if (idx < 0) idx = -idx;
-        if (idx >= F) idx = 2 * (F - 1) - idx;
-        win[k] = row[idx];
-      }
-      for (int a = 1; a < width; ++a) {            // insertion sort (width <= 15)
-        const float t = win[a];
-        int b = a - 1;
-        while (b >= 0 && win[b] > t) { win[b + 1] = win[b]; --b; }
-        win[b + 1] = t;
-      }
-      v = win[pad];
+      float w[WIDTH];
+#pragma unroll
+      for (int k = 0; k < WIDTH; ++k) w[k] = row[idx[k]];
+#pragma unroll
+      for (int round = 0; round < WIDTH; ++round)
+#pragma unroll
+        for (int k = round & 1; k + 1 < WIDTH; k += 2) {
+          const float lo = fminf(w[k], w[k + 1]), hi = fmaxf(w[k], w[k + 1]);
+          w[k] = lo;
+          w[k + 1] = hi;
+        }
+      v = w[PAD];
     }
     acc += v;
   }
@@ -164,7 +176,12 @@ void launch_align_matrix(const float* attn, int S, int nh, int T, int F, int wid
   WM_LAUNCH_CHECK("align_rowsum_kernel");
   hipLaunchKernelGGL(align_norm_kernel, dim3((F + 127) / 128, nh), dim3(128), 0, st, attn, S, nh, T, F, rowsum, z);
   WM_LAUNCH_CHECK("align_norm_kernel");
-  hipLaunchKernelGGL(align_median_kernel, dim3((F + 127) / 128, nrows), dim3(128), 0, st, z, S, nh, F, width, r0, nrows, mat);
+  const dim3 g((F + 127) / 128, nrows), b(128);
+  switch (width) {
+#define MEDW(W_) case W_: hipLaunchKernelGGL(align_median_kernel<W_>, g, b, 0, st, z, S, nh, F, r0, nrows, mat); break;
+    MEDW(1) MEDW(3) MEDW(5) MEDW(7) MEDW(9) MEDW(11) MEDW(13) MEDW(15)
+#undef MEDW
+  }
   WM_LAUNCH_CHECK("align_median_kernel");
 }
 

@@ -618,6 +618,124 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
   }
 }
 
+// Cross-attention WITH capture (word alignment, wm_align_batch's teacher-forced pass): one block per (up to RG
+// rows of one window, head).  The window's K panel is streamed ONCE for the block's rows (pass 1: each 8-lane group
+// takes one key and forms all RG dot products, scores to LDS), each row's softmax is formed in LDS and written out
+// for a captured head, then the V panel streams once (pass 3: every row's weighted sum at once).  The per-(row, head)
+// form (dec_attn_kernel) streamed both panels per row: ~2 TB of L2/MALL reads per 150-window large-v3 alignment.
+template <int RG>
+__global__ __launch_bounds__(256) void cross_capture_kernel(DecAttnArgs a, int group, int bpg) {
+  __shared__ float s_sc[RG][CT_MAX];
+  __shared__ float s_sum[RG];
+  __shared__ float s_acc[4][RG][HD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, sub = lane & 7, kg = tid >> 3;
+  const int H = a.H, T = a.T;
+  const int h = blockIdx.x % H, rb = blockIdx.x / H;
+  const int g = rb / bpg, j = rb - g * bpg;
+  const int r0 = g * group + j * RG, nr = min(RG, group - j * RG);
+  const int hyp0 = a.row_hyp[r0];
+  if (a.done && a.done[hyp0]) return;
+  const long long off = ((long long)a.hyp_slot[hyp0] * H + h) * ((long long)T * HD);
+  const bf16* K = a.kbase + off;
+  const bf16* V = a.vbase + off;
+  if (a.stat && tid == 0) atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), (unsigned long long)(T * 2 * HD * 2 + nr * 2 * HD * 2));
+  float qf[RG][8];
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    if (r < nr) {
+      load8(a.q + (long long)(r0 + r) * a.ldq + h * HD + sub * 8, qf[r]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qf[r][i] *= a.scale_log2;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qf[r][i] = 0.f;
+    }
+  }
+  // pass 1: scores, 32 keys per iteration (one per 8-lane group)
+  for (int kb = 0; kb < T; kb += 32) {
+    const int p = kb + kg;
+    float kf[8];
+    if (p < T) load8(K + (long long)p * HD + sub * 8, kf);
+    else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) kf[i] = 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d = fmaf(qf[r][i], kf[i], d);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      if (sub == 0 && p < T && r < nr) s_sc[r][p] = d;
+    }
+  }
+  __syncthreads();
+  // softmax per row: wave w takes rows w, w + 4, ...
+  for (int r = wv; r < nr; r += 4) {
+    float mx = -INFINITY;
+    for (int p = lane; p < T; p += 64) mx = fmaxf(mx, s_sc[r][p]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int p = lane; p < T; p += 64) {
+      const float e = exp2f(s_sc[r][p] - mx);
+      s_sc[r][p] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) s_sum[r] = sum;
+  }
+  __syncthreads();
+  if (a.probs && a.head_map[h] >= 0) {
+    const int hm = a.head_map[h];
+    for (int r = 0; r < nr; ++r) {
+      const float inv = 1.0f / s_sum[r];
+      float* pr = a.probs + ((long long)(r0 + r) * a.n_align + hm) * T;
+      for (int p = tid; p < T; p += 256) pr[p] = s_sc[r][p] * inv;
+    }
+  }
+  // pass 3: V, every row at once
+  float acc[RG][8];
+#pragma unroll
+  for (int r = 0; r < RG; ++r)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[r][i] = 0.f;
+  for (int kb = 0; kb < T; kb += 32) {
+    const int p = kb + kg;
+    if (p < T) {
+      float vf[8];
+      load8(V + (long long)p * HD + sub * 8, vf);
+#pragma unroll
+      for (int r = 0; r < RG; ++r) {
+        const float w = s_sc[r][p];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[r][i] = fmaf(w, vf[i], acc[r][i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RG; ++r)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc[r][i] += __shfl_xor(acc[r][i], 8, 64);
+      acc[r][i] += __shfl_xor(acc[r][i], 16, 64);
+      acc[r][i] += __shfl_xor(acc[r][i], 32, 64);
+    }
+  if (lane < 8) {
+#pragma unroll
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s_acc[wv][r][sub * 8 + i] = acc[r][i];
+  }
+  __syncthreads();
+  for (int idx = tid; idx < nr * HD; idx += 256) {
+    const int r = idx / HD, e = idx - r * HD;
+    const float v = s_acc[0][r][e] + s_acc[1][r][e] + s_acc[2][r][e] + s_acc[3][r][e];
+    a.out[(long long)(r0 + r) * a.ldo + h * HD + e] = f2bf(v / s_sum[r]);
+  }
+}
+
 static void launch_k(bool self, dim3 grid, const DecAttnArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (ev0) {
     if (self) hipExtLaunchKernelGGL(dec_attn_kernel<true>, grid, dim3(256), 0, st, ev0, ev1, 0, a);
@@ -671,6 +789,15 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
     if (T > CT_MAX) throw std::runtime_error("cross_attn: too many keys for capture");
     if (fz.q_part) throw std::runtime_error("cross_attn: fused q slabs unsupported with capture");
     a.splits = 1;
+    if (group > 1 && rows % group == 0) {
+      constexpr int RG = 8;
+      const int bpg = (group + RG - 1) / RG;
+      const dim3 grid((rows / group) * bpg * H);
+      if (ev0) hipExtLaunchKernelGGL(cross_capture_kernel<RG>, grid, dim3(256), 0, st, ev0, ev1, 0, a, group, bpg);
+      else hipLaunchKernelGGL(cross_capture_kernel<RG>, grid, dim3(256), 0, st, a, group, bpg);
+      WM_LAUNCH_CHECK("cross_capture_kernel");
+      return;
+    }
     launch_k(false, dim3(rows * H, 1), a, st, ev0, ev1);
     WM_LAUNCH_CHECK("dec_attn_kernel<cross>");
     return;

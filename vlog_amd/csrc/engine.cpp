@@ -1583,22 +1583,29 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
   HIP_OK(hipMemGetInfo(&free_b, &total_b));
   const double reusable = (double)e->a_attn.bytes + (double)e->a_logits.bytes;
   const double budget = std::max(1.5e9, std::min(48e9, 0.5 * (double)free_b + reusable));
+  // Items longest-first, chunked so padding (every sequence of a chunk padded to its longest) stays under a
+  // quarter of the chunk's rows: with transcripts of 5 to 220 tokens one padded pass would run ~2x the rows.
+  std::vector<int> ord(n);
+  for (int i = 0; i < n; ++i) ord[i] = i;
+  std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return S[x] > S[y]; });
   int i0 = 0;
   while (i0 < n) {
     int i1 = i0, smax = 0;
-    long long ntext = 0;
+    long long ntext = 0, sum_s = 0;
     while (i1 < n) {
-      const int s2 = std::max(smax, S[i1]);
-      const double bytes = (double)(i1 - i0 + 1) * s2 * n_heads * T * 4 + (double)(ntext + nt[i1]) * V * 4;
-      if (i1 > i0 && bytes > budget) break;
+      const int it = ord[i1];
+      const int s2 = std::max(smax, S[it]);
+      const double bytes = (double)(i1 - i0 + 1) * s2 * n_heads * T * 4 + (double)(ntext + nt[it]) * V * 4;
+      if (i1 > i0 && (bytes > budget || (double)(i1 - i0 + 1) * s2 > 1.25 * (double)(sum_s + S[it]))) break;
       smax = s2;
-      ntext += nt[i1];
+      ntext += nt[it];
+      sum_s += S[it];
       ++i1;
     }
     const int c = i1 - i0;
     std::vector<int> toks((size_t)c * smax, m.eot), slots(c), lrows, next;
     for (int k = 0; k < c; ++k) {
-      const int i = i0 + k;
+      const int i = ord[i0 + k];
       int* t = &toks[(size_t)k * smax];
       for (int j = 0; j < sot_len; ++j) t[j] = h_sot[j];
       t[sot_len] = m.no_timestamps;
@@ -1622,7 +1629,7 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
     std::vector<int> Ns(c), Ms(c);
     long long xt = 0, ct = 0, pt = 0;
     for (int k = 0; k < c; ++k) {
-      const int i = i0 + k;
+      const int i = ord[i0 + k];
       Ns[k] = nt[i] + 1; Ms[k] = F[i];
       xo[k] = xt; co[k] = ct; po[k] = pt;
       xt += (long long)Ns[k] * Ms[k];
@@ -1633,7 +1640,7 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
     e->a_rowsum.ensure((size_t)smax * n_heads * 4);
     e->a_z.ensure((size_t)n_heads * smax * T * 4);
     for (int k = 0; k < c; ++k) {
-      const int i = i0 + k;
+      const int i = ord[i0 + k];
       launch_align_matrix(e->a_attn.as<float>() + (size_t)k * smax * n_heads * T, S[i], n_heads, T, F[i], medw, sot_len,
                           nt[i] + 1, e->a_rowsum.as<float>(), e->a_z.as<float>(), e->a_mat.as<float>() + xo[k], st);
     }
@@ -1657,13 +1664,16 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
     launch_dtw_batch(e->a_mat.as<float>(), d_xo, d_N, d_M, e->a_cost.as<float>(), e->a_trace.as<signed char>(), d_co,
                      e->a_pi.as<int>(), e->a_pj.as<int>(), d_po, e->a_plen.as<int>(), c, st);
     std::vector<int> pi(pt), pj(pt), plen(c);
-    HIP_OK(hipMemcpyAsync(h_probs + h_text_off[i0], e->a_probs.p, ntext * 4, hipMemcpyDeviceToHost, st));
+    std::vector<float> probs(ntext);                // in chunk order: item k's text tokens after item k-1's
+    HIP_OK(hipMemcpyAsync(probs.data(), e->a_probs.p, ntext * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(pi.data(), e->a_pi.p, pt * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(pj.data(), e->a_pj.p, pt * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(plen.data(), e->a_plen.p, c * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    for (int k = 0; k < c; ++k) {
-      const int i = i0 + k;
+    for (int k = 0, pos = 0; k < c; ++k) {
+      const int i = ord[i0 + k];
+      for (int j = 0; j < nt[i]; ++j) h_probs[h_text_off[i] + j] = probs[pos + j];
+      pos += nt[i];
       h_plen[i] = plen[k];
       for (int q = 0; q < plen[k]; ++q) {
         h_pi[h_path_off[i] + q] = pi[po[k] + q];
