@@ -260,6 +260,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "encode_chunk" (default 160): windows per encoder pass inside wm_encode (~52 MB of activation scratch
  *   per large-v3 window).
  *   "cross_fp8" (default 0): opt-in fp8 (OCP e4m3) cross memory in the factored form (changes numerics).
+ *   "cross_tf" (default 1): the teacher-forced passes of wm_align / wm_align_batch (projected form) run the
+ *   cross-attention on the matrix cores (bf16 MFMA, f32 scores and captured probabilities; the attention weights
+ *   enter the V product as bf16); 0 = the f32 VALU kernels of the decode path.
  *   "debug_nan_row" (default -1, TEST ONLY): >= 0 overwrites logits row r of every decode pass of wm_generate with
  *   NaN before token selection (exercises the failure contract of wm_generate). */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);

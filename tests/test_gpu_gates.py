@@ -158,30 +158,40 @@ def test_config5_beam5_identical_to_oracle_beam(lv3):
 def test_config5_alignment_large_v3_vs_oracle(lv3):
     """Config 5's word alignment at large-v3 (128 mels, 20 heads, the alignment heads of the last half of the
     decoder): wm_align_batch over 6 windows vs oracle/align.py on the GPU's encoder output — text-token
-    probabilities, and the DTW path (jumps) identical on >= 99 % of tokens."""
+    probabilities, and the DTW path (jumps) identical on >= 99 % of tokens — in both cross-attention forms: the
+    factored one, and the projected one the product runs for beam groups, whose teacher-forced pass takes the
+    matrix-core kernel (attn_dec.hip cross_tf_kernel, option cross_tf)."""
     from oracle.align import find_alignment
     st = lv3.st
     res = lv3.greedy()
     ws = sample_indices(lv3.W, 6)
     texts = [[t for t in res[w].tokens if t < st.eot] for w in ws]
     heads = lv3.dims.default_alignment_heads()
-    got = lv3.eng.align_batch(ws, lv3.prompt, texts, [3000] * len(ws), heads, median_filter_width=7)
+    refs = [find_alignment(lv3.orc, lv3.orc.cross_kv(lv3.enc_of([w])), lv3.prompt, text, st, 3000, heads, 7)
+            for w, text in zip(ws, texts)]
 
     def jumps(ti, tj):
         return tj[np.pad(np.diff(ti), (1, 0), constant_values=1).astype(bool)] / 50.0
 
-    tok_same, tok_total, pmax = 0, 0, 0.0
-    for w, text, (gp, gi, gj) in zip(ws, texts, got):
-        rp, ri, rj = find_alignment(lv3.orc, lv3.orc.cross_kv(lv3.enc_of([w])), lv3.prompt, text, st, 3000, heads, 7)
-        pmax = max(pmax, float(np.max(np.abs(gp - rp))))
-        ja, jr = jumps(gi, gj), jumps(ri, rj)
-        assert ja.shape == jr.shape
-        tok_same += int(np.sum(np.abs(ja - jr) <= 0.02 + 1e-9))
-        tok_total += ja.size
-    _record("large-v3 alignment vs oracle (6 windows)", dict(tokens_within_20ms=tok_same, tokens=tok_total,
-                                                             max_text_token_prob_diff=pmax))
-    assert pmax < 1e-3
-    assert tok_same >= GATE_IDENTICAL * tok_total, (tok_same, tok_total)
+    try:
+        for form, mode in (("factored", 1), ("projected, MFMA teacher-forced pass", 0)):
+            lv3.eng.set_option("cross_mode", mode)
+            lv3.eng.cross_kv(lv3.enc, 0)
+            assert lv3.eng.option("cross_tf") == 1
+            got = lv3.eng.align_batch(ws, lv3.prompt, texts, [3000] * len(ws), heads, median_filter_width=7)
+            tok_same, tok_total, pmax = 0, 0, 0.0
+            for (gp, gi, gj), (rp, ri, rj) in zip(got, refs):
+                pmax = max(pmax, float(np.max(np.abs(gp - rp))))
+                ja, jr = jumps(gi, gj), jumps(ri, rj)
+                assert ja.shape == jr.shape
+                tok_same += int(np.sum(np.abs(ja - jr) <= 0.02 + 1e-9))
+                tok_total += ja.size
+            _record(f"large-v3 alignment vs oracle (6 windows, {form})",
+                    dict(tokens_within_20ms=tok_same, tokens=tok_total, max_text_token_prob_diff=pmax))
+            assert pmax < 1e-3, form
+            assert tok_same >= GATE_IDENTICAL * tok_total, (form, tok_same, tok_total)
+    finally:
+        lv3.eng.set_option("cross_mode", 1)
 
 
 # ------------------------------------------------------------------------------------------ config 1

@@ -82,6 +82,44 @@ def test_factored_alignment_capture(small_models):
     assert np.abs(b - ref).max() < 2e-3
 
 
+def test_teacher_forced_mfma_cross_attention(small_models):
+    """The alignment pass's matrix-core cross-attention (attn_dec.hip cross_tf_kernel, projected form, option
+    cross_tf) against the decode path's f32 VALU kernels and the f32 oracle: three windows x 150 rows (two 128-row
+    tiles per window, the second partial), every alignment head captured, every other head on the one-pass form.
+    Probabilities (f32, exactly normalised by the kernel's first pass) within 2e-3 of the oracle, logits within
+    2 % of the scale."""
+    dims, eng, enc, orc, W = small_models
+    st = dims.specials
+    heads = dims.default_alignment_heads()
+    S = 150
+    toks = np.array([[st.sot, st.lang_token("en"), st.transcribe, st.no_timestamps] +
+                     list(range(2000 + 37 * i, 2000 + 37 * i + S - 5)) + [st.eot] for i in range(3)])
+    eng.set_option("cross_mode", 0)
+    eng.reserve(W, 8)
+    eng.cross_kv(enc, 0)
+    out = {}
+    try:
+        for tf in (1, 0):
+            eng.set_option("cross_tf", tf)
+            lg, at = eng.forward([0, 3, 1], toks, align_heads=heads)
+            out[tf] = (lg.cpu().numpy(), at.cpu().numpy())
+    finally:
+        eng.set_option("cross_tf", 1)
+        eng.set_option("cross_mode", 1)
+        eng.reserve(W, 8)
+        eng.cross_kv(enc, 0)
+    (la, aa), (lb, ab) = out[1], out[0]
+    assert np.all(np.isfinite(aa)) and np.allclose(aa.sum(-1), 1.0, atol=1e-4)
+    assert np.abs(aa - ab).max() < 2e-3, np.abs(aa - ab).max()
+    assert np.abs(la - lb).max() < 0.02 * max(np.abs(lb).max(), 1.0)
+    encf = enc.float().cpu().numpy()
+    for i, w in enumerate((0, 3, 1)):
+        ref, _, cw = orc.decode(toks[i:i + 1], orc.cross_kv(encf[w:w + 1]), return_cross_attn=True)
+        r = np.stack([cw[l][0, h] for l, h in heads], 1)
+        assert np.abs(aa[i] - r).max() < 2e-3
+        assert np.abs(la[i] - ref[0]).max() < 0.02 * np.abs(ref).max() + 1e-3
+
+
 @pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0)], ids=["greedy", "beam5"])
 def test_factored_generate_matches_projected(small_models, kw):
     dims, eng, enc, orc, W = small_models

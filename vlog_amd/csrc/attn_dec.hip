@@ -736,6 +736,222 @@ __global__ __launch_bounds__(256) void cross_capture_kernel(DecAttnArgs a, int g
   }
 }
 
+// ------------------------------------------------------------------------------------------------------
+// Cross-attention of a TEACHER-FORCED pass (wm_align_batch / wm_forward with capture: `group` rows of one window,
+// up to ~220, against its 1500 keys) on the matrix cores.  The VALU kernels above do ~2 x 64 FMAs per (row, key)
+// per head: at 150 windows x ~100 rows x 32 layers that is ~3.7 TFLOP of f32 FMA (~260 ms), while the K/V panels
+// are only 1.15 GB per layer.  Here one block = 128 rows (4 waves x 32) of one (window, head): the window's K/V
+// panels stream through LDS once per block, S^T = K . Q^T and O^T += V^T . P^T on 32x32x16 bf16 MFMA with the
+// encoder kernel's fragment layouts and LDS swizzles (attn_enc.hip attn_enc_v2_kernel).  Differences from it:
+// q is used as stored (exact bf16) and the f32 scores are scaled after the MFMA; for a CAPTURED head (head_map >= 0)
+// a first pass over K alone forms each row's exact max and sum, so the second pass writes the normalised f32
+// probabilities (p = exp2(s - m) / l, as the VALU capture kernel) and accumulates O with the final max (no rescale).
+// Uncaptured heads take one pass with the online softmax and deferred rescale.
+typedef __attribute__((ext_vector_type(4))) short tf_i16x4;
+typedef __attribute__((ext_vector_type(2))) int tf_i32x2;
+#define TF_KT 64
+#define TF_THR 8.0f
+__device__ __forceinline__ int tf_kslot(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 7)) << 3); }
+__device__ __forceinline__ int tf_vslot(int r, int c) { return r * 64 + ((c ^ (((r >> 1) & 1) << 2)) << 3); }
+
+__global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int group, int nqt) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TF_KT * HD];     // [buf][K | V][64 keys][64]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ql = lane & 31, hh = lane >> 5;
+  const int H = a.H, T = a.T;
+  int qt, h, g;
+  {
+    // XCD-aware: the row tiles of one (window, head) get consecutive remapped ids (one XCD's L2 holds the panels)
+    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    qt = wgid % nqt;
+    const int rest = wgid / nqt;
+    h = rest % H;
+    g = rest / H;
+  }
+  const int row0 = g * group;
+  const int hyp0 = a.row_hyp[row0];
+  if (a.done && a.done[hyp0]) return;
+  const long long off = ((long long)a.hyp_slot[hyp0] * H + h) * ((long long)T * HD);
+  const bf16* K = a.kbase + off;
+  const bf16* V = a.vbase + off;
+  const int hm = a.probs ? a.head_map[h] : -1;
+  const bool cap = hm >= 0;
+  if (a.stat && tid == 0)
+    atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), (unsigned long long)((cap ? 3 : 2) * T * HD * 2));
+  const int r = qt * 128 + wv * 32 + ql;
+  const bool valid = r < group;
+  bf16x8 qf[4];
+  {
+    const bf16* qp = a.q + (long long)(row0 + min(r, group - 1)) * a.ldq + h * HD + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  }
+  const float sl2 = a.scale_log2;
+  const int nt = (T + TF_KT - 1) / TF_KT;
+  i32x4 rk[2], rv[2];
+  auto load_tile = [&](int t, bool withv) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * 256, key = min(t * TF_KT + (c >> 3), T - 1), ch = c & 7;
+      rk[i] = __builtin_nontemporal_load((const i32x4*)(K + (long long)key * HD + ch * 8));
+      if (withv) rv[i] = __builtin_nontemporal_load((const i32x4*)(V + (long long)key * HD + ch * 8));
+    }
+  };
+  auto store_tile = [&](int buf, bool withv) {
+    bf16* sK = smem + buf * (2 * TF_KT * HD);
+    bf16* sV = sK + TF_KT * HD;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * 256, rr = c >> 3, ch = c & 7;
+      *(i32x4*)(sK + tf_kslot(rr, ch)) = rk[i];
+      if (withv) *(i32x4*)(sV + tf_vslot(rr, ch)) = rv[i];
+    }
+  };
+  // S^T of the tile's two 32-key blocks, scaled to log2 units, keys past T masked
+  auto scores = [&](const bf16* sK, int t, f32x16 (&sc)[2]) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sc[kb][e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 ka = *(const bf16x8*)(sK + tf_kslot(kb * 32 + ql, 2 * s + hh));
+        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sc[kb], 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int key = t * TF_KT + kb * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
+        sc[kb][e] = key < T ? sc[kb][e] * sl2 : -INFINITY;
+      }
+    }
+  };
+
+  float m_run = -INFINITY, l_run = 0.f;
+  if (cap) {
+    // pass 1: exact row max and sum from K alone (lane-local partials over the lane's half of the keys)
+    load_tile(0, false);
+    store_tile(0, false);
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const bf16* sK = smem + (t & 1) * (2 * TF_KT * HD);
+      if (t + 1 < nt) load_tile(t + 1, false);
+      f32x16 sc[2];
+      scores(sK, t, sc);
+      float mx = m_run;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sc[kb][e]);
+      float acc = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc += exp2f(sc[kb][e] - mx);
+      l_run = l_run * exp2f(m_run - mx) + acc;     // mx is finite: every tile holds a key < T
+      m_run = mx;
+      if (t + 1 < nt) store_tile((t + 1) & 1, false);
+      __syncthreads();
+    }
+    const float mo = __shfl_xor(m_run, 32, 64), lo = __shfl_xor(l_run, 32, 64);
+    const float M = fmaxf(m_run, mo);
+    l_run = l_run * exp2f(m_run - M) + lo * exp2f(mo - M);
+    m_run = M;
+  }
+  const float inv_cap = cap ? 1.0f / l_run : 0.f;
+  float* prow = cap && valid ? a.probs + ((long long)(row0 + r) * a.n_align + hm) * T : nullptr;
+
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[i][e] = 0.f;
+  load_tile(0, true);
+  store_tile(0, true);
+  __syncthreads();
+  const int G = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;    // tr_b16: group, row q, col block p
+  for (int t = 0; t < nt; ++t) {
+    const bf16* sK = smem + (t & 1) * (2 * TF_KT * HD);
+    const bf16* sV = sK + TF_KT * HD;
+    if (t + 1 < nt) load_tile(t + 1, true);
+    f32x16 sc[2];
+    scores(sK, t, sc);
+    if (!cap) {
+      float mx = sc[0][0];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sc[kb][e]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (__any(mx > m_run + TF_THR)) {
+        const float mn = fmaxf(m_run, mx);
+        const float alpha = exp2f(m_run - mn);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) o[i][e] *= alpha;
+        m_run = mn;
+      }
+    }
+    bf16x8 pf[2][2];                                    // [key block][k-step]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float pv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        pv[e] = exp2f(sc[kb][e] - m_run);
+        if (!cap) l_run += pv[e];
+        pf[kb][e >> 3][e & 7] = f2bf(pv[e]);
+      }
+      if (prow) {
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int key = t * TF_KT + kb * 32 + 8 * gg + 4 * hh;
+          if (key < T)
+            *(f32x4*)(prow + key) = f32x4{pv[4 * gg] * inv_cap, pv[4 * gg + 1] * inv_cap, pv[4 * gg + 2] * inv_cap,
+                                          pv[4 * gg + 3] * inv_cap};
+        }
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+          tf_i32x2 vw[2];
+#pragma unroll
+          for (int jh = 0; jh < 2; ++jh) {
+            const int row = kb * 32 + 16 * s + 8 * jh + 4 * (G >> 1) + gq;
+            const int col = 32 * hb + 16 * (G & 1) + 4 * gp;
+            const bf16* ad = sV + tf_vslot(row, col >> 3) + (col & 7);
+            // (whole-register bit casts, as attn_enc.hip: an element-wise insert miscompiles on ROCm 7.2)
+            vw[jh] = __builtin_bit_cast(tf_i32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                      (__attribute__((address_space(3))) tf_i16x4*)(ad)));
+          }
+          const bf16x8 va = __builtin_bit_cast(bf16x8, i32x4{vw[0][0], vw[0][1], vw[1][0], vw[1][1]});
+          o[hb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[kb][s], o[hb], 0, 0, 0);
+        }
+    if (t + 1 < nt) store_tile((t + 1) & 1, true);
+    __syncthreads();
+  }
+  if (!cap) l_run += __shfl_xor(l_run, 32, 64);
+  if (valid) {
+    const float inv = cap ? inv_cap : 1.0f / l_run;
+    bf16* orow = a.out + (long long)(row0 + r) * a.ldo + h * HD;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[hb][4 * gg + e] * inv);
+        *(bf16x4*)(orow + 32 * hb + 8 * gg + 4 * hh) = w;
+      }
+  }
+}
+
 static void launch_k(bool self, dim3 grid, const DecAttnArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (ev0) {
     if (self) hipExtLaunchKernelGGL(dec_attn_kernel<true>, grid, dim3(256), 0, st, ev0, ev1, 0, a);
@@ -785,6 +1001,17 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
   a.out = out; a.ldo = ldo; a.H = H; a.T = T; a.n_ctx = T;
   a.part_m = part_m; a.part_l = part_l; a.part_o = part_o; a.probs = probs; a.head_map = head_map; a.n_align = n_align;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;
+  if (fz.tf && group >= 16 && rows % group == 0 && !fz.q_part) {
+    if (probs && !head_map) throw std::runtime_error("cross_attn: capture without a head map");
+    a.splits = 1;
+    const int nqt = (group + 127) / 128;
+    const long long nblk = (long long)(rows / group) * H * nqt;
+    if (nblk > (1LL << 31) - 1) throw std::runtime_error("cross_attn: grid too large");
+    if (ev0) hipExtLaunchKernelGGL(cross_tf_kernel, dim3((unsigned)nblk), dim3(256), 0, st, ev0, ev1, 0, a, group, nqt);
+    else hipLaunchKernelGGL(cross_tf_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a, group, nqt);
+    WM_LAUNCH_CHECK("cross_tf_kernel");
+    return;
+  }
   if (probs) {        // attention capture (word alignment): the two-pass kernel keeps the probabilities
     if (T > CT_MAX) throw std::runtime_error("cross_attn: too many keys for capture");
     if (fz.q_part) throw std::runtime_error("cross_attn: fused q slabs unsupported with capture");

@@ -60,6 +60,7 @@ struct CrossFuse {
   int q_splits = 0, q_rows = 0;
   const float* q_bias = nullptr;
   int* cnt = nullptr;              // >= rows*H zeroed ints (nullptr: separate combine kernel)
+  int tf = 0;                      // teacher-forced pass (`group` contiguous rows per window): matrix-core kernel
 };
 
 // Launch check used by every host-side launcher: converts an asynchronous launch failure into an

@@ -193,6 +193,7 @@ struct wm_engine {
   // holds its encoder output, 3.84 MB for large-v3), 0 = projected cross-KV panels (attn_dec.hip: 245.8 MB
   // per large-v3 window, projected by wm_cross_kv)
   int cross_mode = 1;
+  int cross_tf = 1;          // teacher-forced passes (alignment) run the projected form's cross-attention on MFMA
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
                              // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
@@ -598,6 +599,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     gemm(DEC_CQ, ln_fuse ? ln_operand(W.ln2_w, W.ln2_b) : amat(hb, d), W.cq_w, d, d, d, ep);
   }
   if ((e->cross_fuse & 2) && e->cross_mode == 0) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
+  fz.tf = (attn && align_map && e->cross_tf) ? 1 : 0;
   float* probs = nullptr;
   const int* hmap = nullptr;
   if (attn && align_map) {
@@ -2075,6 +2077,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
       }
     }
     else if (k == "debug_nan_row") e->dbg_nan_row = (int)std::max<int64_t>(-1, std::min<int64_t>(value, 1 << 30));
+    else if (k == "cross_tf") e->cross_tf = value ? 1 : 0;
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }
@@ -2113,6 +2116,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_fp8") *value = e->cross_fp8;
     else if (k == "cross_mode") *value = e->cross_mode;
     else if (k == "debug_nan_row") *value = e->dbg_nan_row;
+    else if (k == "cross_tf") *value = e->cross_tf;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
   });
 }
