@@ -82,10 +82,12 @@ def test_factored_alignment_capture(small_models):
     assert np.abs(b - ref).max() < 2e-3
 
 
-def test_teacher_forced_mfma_cross_attention(small_models):
-    """The alignment pass's matrix-core cross-attention (attn_dec.hip cross_tf_kernel, projected form, option
-    cross_tf) against the decode path's f32 VALU kernels and the f32 oracle: three windows x 150 rows (two 128-row
-    tiles per window, the second partial), every alignment head captured, every other head on the one-pass form.
+@pytest.mark.parametrize("mode", [0, 1], ids=["projected", "factored"])
+def test_teacher_forced_mfma_cross_attention(small_models, mode):
+    """The alignment pass's matrix-core cross-attention (attn_dec.hip cross_tf_kernel, option cross_tf) against the
+    decode path's kernels of the same form and the f32 oracle: three windows x 150 rows (two 128-row tiles per
+    window, the second partial), every alignment head captured, every other head on the one-pass form.  In the
+    factored form the pass first projects each layer's K/V panels of its windows (wm_cross_kv's GEMM, one layer).
     Probabilities (f32, exactly normalised by the kernel's first pass) within 2e-3 of the oracle, logits within
     2 % of the scale."""
     dims, eng, enc, orc, W = small_models
@@ -94,7 +96,7 @@ def test_teacher_forced_mfma_cross_attention(small_models):
     S = 150
     toks = np.array([[st.sot, st.lang_token("en"), st.transcribe, st.no_timestamps] +
                      list(range(2000 + 37 * i, 2000 + 37 * i + S - 5)) + [st.eot] for i in range(3)])
-    eng.set_option("cross_mode", 0)
+    eng.set_option("cross_mode", mode)
     eng.reserve(W, 8)
     eng.cross_kv(enc, 0)
     out = {}

@@ -772,7 +772,10 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
   const int row0 = g * group;
   const int hyp0 = a.row_hyp[row0];
   if (a.done && a.done[hyp0]) return;
-  const long long off = ((long long)a.hyp_slot[hyp0] * H + h) * ((long long)T * HD);
+  // panels by window slot; without a slot table (the factored form's per-layer projection of the pass's windows)
+  // by the pass's window index
+  const int slot = a.hyp_slot ? a.hyp_slot[hyp0] : hyp0;
+  const long long off = ((long long)slot * H + h) * ((long long)T * HD);
   const bf16* K = a.kbase + off;
   const bf16* V = a.vbase + off;
   const int hm = a.probs ? a.head_map[h] : -1;
@@ -1012,6 +1015,7 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
     WM_LAUNCH_CHECK("cross_tf_kernel");
     return;
   }
+  if (!hyp_slot) throw std::runtime_error("cross_attn: no slot table outside the teacher-forced kernel");
   if (probs) {        // attention capture (word alignment): the two-pass kernel keeps the probabilities
     if (T > CT_MAX) throw std::runtime_error("cross_attn: too many keys for capture");
     if (fz.q_part) throw std::runtime_error("cross_attn: fused q slabs unsupported with capture");

@@ -209,6 +209,10 @@ struct wm_engine {
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
   std::vector<DecLayerW> dec_w;
+  // factored form, teacher-forced alignment pass: the pass's windows' encoder outputs gathered contiguously, and one
+  // layer's projected K/V panels of them [2][tf_nwin][H][T][64] (re-projected per layer on MFMA)
+  DevBuf a_enc, a_kv;
+  int tf_nwin = 0;
   DevBuf a_logits, a_attn, a_next, a_probs, a_rowsum, a_z, a_mat, a_cost, a_trace, a_pi, a_pj, a_plen, a_meta;
   DevBuf prof_dbytes;        // device counters (attention kernels add the bytes they actually read)
   hipEvent_t ev_get() {
@@ -613,7 +617,23 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     }
   }
   if (mid) HIP_OK(hipEventRecord(mid, st));
-  if (e->cross_mode == 1) {
+  if (e->cross_mode == 1 && e->tf_nwin > 0 && attn && align_map) {
+    // factored form, alignment pass: this layer's K/V panels of the pass's windows projected on MFMA (the wm_cross_kv
+    // GEMM restricted to one layer: 2 x d x d x T flops per window), then the projected form's teacher-forced kernel
+    // over them (window = hypothesis index of the pass).  ~2.5x fewer flops than the factored attention at ~100
+    // rows per window, and all of it on the matrix cores.
+    const int nw = e->tf_nwin;
+    GemmEpi ep = epi_of(EPI_CROSS_KV, e->a_kv.p, 0, e->Wf("dec.ckv.b") + (size_t)l * 2 * d);
+    ep.rpb = T; ep.d = d; ep.head_dim = 64; ep.n_head = H; ep.n_slots = nw; ep.slot0 = 0;
+    gemm_p(e, P_CROSSKV_GEMM, amat(e->a_enc.as<bf16>(), d), e->Wb("dec.ckv.w") + (size_t)l * 2 * d * d, d, nw * T, 2 * d, d,
+           ep, st);
+    const bf16* kv = e->a_kv.as<bf16>();
+    const size_t po = (size_t)r0 * H * 16;
+    ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
+    launch_cross_attn(q, d, kv, kv + (size_t)nw * H * T * 64, T, nullptr, row_hyp, done, ao, d, rows, H, cross_group,
+                      e->s_pm.as<float>() + po, e->s_pl.as<float>() + po, e->s_po.as<float>() + po * 64, probs, hmap,
+                      n_align, sl.total_rows, e->cross_cap, fz, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+  } else if (e->cross_mode == 1) {
     // factored: q' = Wk_h^T q_h, attention over the encoder output, split merge + Wv_h (attn_xenc.hip)
     const int splits = xattn_splits(sl.total_rows, cross_group, H, T, d);
     const size_t prow = (size_t)H * d;
@@ -1501,6 +1521,20 @@ void forward(wm_engine* e, int n_seq, const int* h_slots, int S, const int* h_to
   HIP_OK(hipMemcpyAsync(e->d_logit_rows.p, lr.data(), nlog * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_hyp_slot.p, hs.data(), n_seq * 4, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(e->d_lin.p, lin.data(), lin.size() * 4, hipMemcpyHostToDevice, st));
+  // factored form with capture (alignment): gather the windows' encoder outputs for the per-layer K/V projection
+  // (decoder_layer); the rows of a window must reach the teacher-forced kernel (S >= 16, launch_cross_attn)
+  e->tf_nwin = 0;
+  if (n_align && e->cross_mode == 1 && e->cross_tf && !e->cross_fp8 && S >= 16) {
+    const int T = m.n_audio_ctx, d = m.n_state;
+    const size_t per = (size_t)T * d;
+    e->a_enc.ensure((size_t)n_seq * per * 2);
+    e->a_kv.ensure((size_t)2 * n_seq * per * 2);
+    for (int s = 0; s < n_seq; ++s)
+      HIP_OK(hipMemcpyAsync(e->a_enc.as<bf16>() + (size_t)s * per, e->xenc.as<bf16>() + (size_t)hs[s] * per, per * 2,
+                            hipMemcpyDeviceToDevice, st));
+    e->tf_nwin = n_seq;
+  }
+  struct TfReset { wm_engine* e; ~TfReset() { e->tf_nwin = 0; } } tf_reset{e};
   decoder_pass(e, rows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_prow_hyp.as<int>(), nullptr,
                e->d_lin.as<int>(), e->d_logit_rows.as<int>(), nlog, d_logits, n_align ? &amap : nullptr, n_align,
                n_align ? d_attn : nullptr, S, st);
@@ -1784,7 +1818,7 @@ void wm_destroy(wm_engine* e) {
                     &e->s_hb, &e->s_q, &e->s_ao, &e->s_ff, &e->s_logits, &e->s_pm, &e->s_pl, &e->s_po, &e->gemm_ws, &e->gemm_ws2, &e->prof_dbytes, &e->d_cross_cnt, &e->d_lnstat,
                     &e->xenc, &e->xscale, &e->xwkt, &e->xwvb, &e->s_qp, &e->s_pu, &e->s_pml, &e->a_logits, &e->a_attn,
                     &e->a_next, &e->a_probs, &e->a_rowsum, &e->a_z, &e->a_mat, &e->a_cost, &e->a_trace, &e->a_pi,
-                    &e->a_pj, &e->a_plen, &e->a_meta, &e->d_tok_lp, &e->d_tok_lp_o, &e->d_fin_lp, &e->d_win_prompt,
+                    &e->a_pj, &e->a_plen, &e->a_meta, &e->a_enc, &e->a_kv, &e->d_tok_lp, &e->d_tok_lp_o, &e->d_fin_lp, &e->d_win_prompt,
                     &e->d_win_slot, &e->d_hyp_out, &e->d_res_tok, &e->d_res_len, &e->d_res_cum, &e->d_res_ns, &e->d_res_lp,
                     &e->d_res_lp_o, &e->d_ev})
     b->release();
