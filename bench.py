@@ -135,9 +135,10 @@ class Pipeline:
             for w, r in zip(order, out):
                 res[w] = r
         else:
+            # beam: with the row-set option, finished windows' hypotheses leave the passes (beam compaction)
             res, steps = eng.generate(list(range(W)), [self.prompt] * W, beam_size=self.beam,
                                       suppress_tokens=self.suppress, max_length=448, check_every=self.check_every,
-                                      stats=gen_stats)
+                                      compact=self.max_rows >= 0, stats=gen_stats)
         t3 = time.perf_counter()
         groups = []
         for w, r in enumerate(res):

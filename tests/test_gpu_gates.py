@@ -257,3 +257,40 @@ def test_config4_variable_length_gates_and_row_set_decode(lv3_var):
         active_row_fraction_all_rows=float(sum(n + 1 for n in lens) / (steps_all * cfg.W)),
         active_row_fraction_row_set=float(sum(n + 1 for n in lens) / max(1, st["row_steps"]))))
     assert same == cfg.W, same
+
+
+def test_config5_beam_compaction_variable_length(lv3_var):
+    """Config 5's search on the variable-length model: beam 5 over 60 windows with the hypotheses of finished
+    windows dropped from the passes (wm_generate compact, beam) vs the all-rows beam decode: the same hypothesis
+    on every window (the model is decisive; the routes differ only in f32 rounding), scores within f32 rounding,
+    and fewer row-steps; 4 windows re-decoded by the oracle's own beam search."""
+    cfg = lv3_var
+    W = 60
+    cfg.eng.reserve(cfg.W, W * 5)
+    cfg.eng.set_option("cross_mode", 0)             # the product's form for beam groups (transcribe.py)
+    try:
+        cfg.eng.cross_kv(cfg.enc, 0)
+        out = {}
+        for compact in (False, True):
+            st = {}
+            res, steps = cfg.eng.generate(list(range(W)), [cfg.prompt] * W, beam_size=5, patience=1.0,
+                                          suppress_tokens=cfg.sup, max_length=448, check_every=4, compact=compact,
+                                          stats=st)
+            out[compact] = (res, steps, st)
+    finally:
+        cfg.eng.set_option("cross_mode", 1)
+    (ra, sa, ta), (rb, sb, tb) = out[False], out[True]
+    same = sum(a.tokens == b.tokens for a, b in zip(ra, rb))
+    lens = [len(r.tokens) for r in ra]
+    ws = sample_indices(W, 4)
+    refs = beam_many(cfg.orc, cfg.orc.cross_kv(cfg.enc_of(ws)), cfg.prompt, cfg.st, cfg.opt(beam=5))
+    oracle_same = sum(r.tokens == list(rb[w].tokens) for w, r in zip(ws, refs))
+    _record("beam5 compaction large-v3 variable-length 60 windows", dict(
+        same_tokens=same, oracle_beam_identical=oracle_same, steps=(sa, sb), row_steps=(ta["row_steps"], tb["row_steps"]),
+        lengths_min_max=(min(lens), max(lens))))
+    assert same == W, same
+    assert oracle_same == len(ws), oracle_same
+    for a, b in zip(ra, rb):
+        assert abs(a.score - b.score) <= 1e-3 * max(1.0, abs(a.score))
+        assert abs(a.no_speech_prob - b.no_speech_prob) < 1e-4
+    assert tb["row_steps"] < ta["row_steps"], (ta, tb)

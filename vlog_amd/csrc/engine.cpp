@@ -1058,40 +1058,78 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     HIP_OK(hipStreamWaitEvent(e->gst, e->ev_g0, 0));
     ds = e->gst;
   }
+  // Beam compaction (a->compact): once the live windows' hypotheses fill <= 5/8 of the pass, the pass keeps only
+  // them (row r -> hypothesis row_hyp[r], window groups stay contiguous); the beam state stays where it is, per
+  // hypothesis (KV cache, lineage, tokens), so the rows' tokens / positions are gathered per pass (rows_fill) and
+  // the selection reads its logits row by row.  Finished windows then stop costing GEMM rows in the tail.
+  int nrows = NH;
+  const bool bcompact = beam && a->compact;
+  std::vector<int> h_rows(NH), h_bdone;
+  for (int h = 0; h < NH; ++h) h_rows[h] = h;
   auto step_eager = [&](int step, hipStream_t s) {
     // logits rows of a decode step are the hypotheses themselves
     // greedy / sampling never reorder hypotheses: the lineage table is the identity and self-attention
     // reads each row's own cache directly (no dependent lineage load per key block)
-    decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                 beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, s, err);
+    if (nrows < NH) {
+      launch_rows_fill(nrows, e->d_row_hyp.as<int>(), e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(),
+                       e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), s);
+      decoder_pass(e, nrows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
+                   e->d_lin.as<int>(), nullptr, nrows, logits, nullptr, 0, nullptr, per, s, err);
+    } else {
+      decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
+                   beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, s, err);
+    }
     sp.step = step;
-    debug_nan(e, logits, NH, s);
-    launch_logits_select(sp, NH, s);
+    debug_nan(e, logits, nrows, s);
+    ProfScope ps(e, P_SELECT, s);
+    launch_logits_select(sp, nrows, s);
     if (beam) launch_beam_select(bp, W, s);
   };
   StepGraph graph;
   int poll[4] = {0, 0, 0, 0};                   // live count + error word
+  bool eager_next = false;                      // the pass after a compaction runs eagerly (sizes scratch), then captures
+  if (bcompact) h_bdone.resize(NH);
   try {
     for (int step = 1; step < max_steps; ++step) {
       if ((step - 1) % check == 0) {
         HIP_OK(hipMemcpyAsync(poll, e->d_n_active.p, sizeof(poll), hipMemcpyDeviceToHost, ds));
+        if (bcompact) HIP_OK(hipMemcpyAsync(h_bdone.data(), e->d_done.p, (size_t)NH * 4, hipMemcpyDeviceToHost, ds));
         HIP_OK(hipStreamSynchronize(ds));
         check_decode_error(poll + 1);
         if (poll[0] <= 0) break;
-      }
-      if (!use_graph || step == 1) {
-        if (use_graph) step_eager(step, ds);
-        else {
-          decoder_pass(e, NH, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
-                       beam ? e->d_lin.as<int>() : nullptr, nullptr, NH, logits, nullptr, 0, nullptr, per, st, err);
-          select(step);
+        // (beam passes are GEMM-row-bound at hundreds of rows, unlike the latency-bound greedy passes: compact at 7/8)
+        if (bcompact && poll[0] * 8 <= nrows * 7) {
+          // a finished window's hypotheses are all done (beam_select); keep the live windows' groups in order
+          int n = 0;
+          for (int r = 0; r < nrows; r += per) {
+            const int h0 = h_rows[r];
+            if (h_bdone[h0]) continue;
+            for (int b = 0; b < per; ++b) h_rows[n + b] = h0 + b;
+            n += per;
+          }
+          if (n > 0 && n < nrows) {
+            nrows = n;
+            HIP_OK(hipMemcpyAsync(e->d_row_hyp.p, h_rows.data(), (size_t)nrows * 4, hipMemcpyHostToDevice, ds));
+            HIP_OK(hipStreamSynchronize(ds));
+            sp.row_hyp = e->d_row_hyp.as<int>();
+            graph.drop();
+            eager_next = true;
+          }
         }
+      }
+      if (!graph.valid()) {                     // a buffer moved since the capture: one eager pass re-sizes
+        graph.drop();
+        eager_next = true;
+      }
+      if (!use_graph || step == 1 || eager_next) {
+        eager_next = false;
+        step_eager(step, use_graph ? ds : st);
       } else {
         if (!graph.exec) ++captures;
         graph.run(ds, [&] { step_eager(step, ds); });
       }
       ++steps;
-      row_steps += NH;
+      row_steps += nrows;
     }
   } catch (...) {
     graph.abort(ds);

@@ -278,7 +278,8 @@ class GpuEngine:
                  sot_index: Optional[int] = None, check_every: int = 4, max_rows: int = 0, compact: bool = False,
                  record_logprobs: bool = False, stats: Optional[dict] = None) -> Tuple[List[GenResult], int]:
         """ctranslate2 Whisper.generate over windows in slots (wm_generate).  max_rows / compact: the row-set decode
-        (greedy / one sampled hypothesis; windows refill finished rows in the given order, include/whisper_mi355.h).
+        (greedy / one sampled hypothesis; windows refill finished rows in the given order, include/whisper_mi355.h);
+        beam search with compact drops finished windows' hypotheses from the passes.
         record_logprobs: per-step log-prob records in each GenResult.  stats: filled with the decode's counters."""
         W = len(slots)
         P = len(prompts[0])

@@ -759,7 +759,7 @@ class BatchedInferencePipeline:
                         temperature=T, num_hypotheses=options.best_of if sampling else 1, seed=seed + 7919 * ti + b0,
                         suppress_tokens=options.suppress_tokens, suppress_blank=options.suppress_blank,
                         max_initial_timestamp_index=mit, with_timestamps=not options.without_timestamps,
-                        sot_index=prompt.index(st.sot), check_every=4)
+                        sot_index=prompt.index(st.sot), check_every=4, compact=True)
                     still = []
                     for i, r in zip(pending, res):
                         alp = segs.avg_logprob(r.score, len(r.tokens), options.length_penalty)
