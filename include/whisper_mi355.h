@@ -234,8 +234,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_gemv" (default 1): passes of <= 32 decoder rows (one window's beam, a few windows) run every
  *   projection on the small-M weight-streaming GEMM (gemm_dec.hip gemv_dec_kernel); it agrees with the other
  *   routes to f32 rounding.  "decode_gemv_ln" (default 1): passes of <= 16 rows compute the LayerNorms after the
- *   out and cout projections inside the cq / fc1 GEMMs (from the residual and per-tile row sums the producers
- *   write) instead of two combine launches per layer; agrees with the unfused form to f32 rounding.
+ *   out and cout projections inside the cq / fc1 GEMMs (from the residual and the per-tile row sums and sums of
+ *   squares about the tile means that the producers write: a two-pass-equivalent variance) instead of two combine
+ *   launches per layer; agrees with the unfused form to f32 rounding.
  *   "decode_ring_gemm" (default 1): 0 disables the all-rows ring GEMM (plan value 0 below falls back to the
  *   split-K skinny GEMM).
  *   "decode_gemm_plan" (default 1): preset routing of the six decoder projections (qkv, out, cq, cout, fc1, fc2)

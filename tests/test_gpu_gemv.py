@@ -55,7 +55,7 @@ def test_gemv_route_vs_oracle_and_general_route(setup, ws, beam):
     b = _gen(eng, enc, tok, ws, beam, 0)
     c = _gen(eng, enc, tok, ws, beam, 1, gemv_ln=0)        # LayerNorm combine launches instead of the fused form
     assert [r.tokens for r in a] == [r.tokens for r in b] == [r.tokens for r in c]
-    # the fused LayerNorm's statistics are summed in another order (single-pass variance): f32-rounding agreement
+    # the fused LayerNorm merges per-tile statistics (another summation order): f32-rounding agreement
     assert max(abs(x.score - y.score) for x, y in zip(a, c)) < 2e-3
     encf = enc.float().cpu().numpy()
     opt = GenerateOptions(beam_size=beam, suppress_tokens=list(tok.suppressed_tokens([-1])), max_length=448)
@@ -65,3 +65,18 @@ def test_gemv_route_vs_oracle_and_general_route(setup, ws, beam):
     if beam > 1:
         refs = beam_many(orc, orc.cross_kv(encf[ws]), list(tok.sot_sequence), dims.specials, opt)
         assert [r.tokens for r in refs] == [r.tokens for r in a]
+
+
+def test_gemv_check_fused_layernorm_statistics():
+    """tools/gemv_check (built in-tree by the library's Makefile): the small-M residual producer's per-tile row
+    statistics (sum, and sum of squares about the tile mean) and the LayerNorm-consuming operand, in isolation
+    against a CPU reference, with canary guards around every buffer — including a residual with a common offset of
+    1000 (|mean| / std ~ 580), where a one-pass E[x^2] - mean^2 variance would lose its digits in f32."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gemv_check")
+    if not os.path.exists(exe):
+        pytest.skip("tools/gemv_check not built (make -C vlog_amd/csrc ../../tools/gemv_check)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0 and "all ok" in r.stdout, r.stdout + r.stderr

@@ -60,12 +60,15 @@ int main() {
   std::mt19937 rng(7);
   std::uniform_real_distribution<float> U(-1.f, 1.f);
   int fails = 0;
+  // offset: a common offset on the residual (|mean| / std ~ 0 and ~ 580), the case where a one-pass E[x^2] - mean^2
+  // variance loses its digits in f32; the statistics are sums and squares about each tile's mean
+  for (float offset : {0.f, 1000.f})
   for (int d : {384, 1280})
     for (int M : {5, 8, 16}) {
       const int N4 = 4 * d;
       std::vector<float> x(M * d), bias(d), g(d), b(d);
       std::vector<uint16_t> ao(M * d), W(d * d), W1((size_t)N4 * d);
-      for (auto& v : x) v = 3.f * U(rng);
+      for (auto& v : x) v = offset + 3.f * U(rng);
       for (auto& v : bias) v = 0.1f * U(rng);
       for (auto& v : g) v = 1.f + 0.2f * U(rng);
       for (auto& v : b) v = 0.1f * U(rng);
@@ -130,13 +133,15 @@ int main() {
       std::vector<uint16_t> og((size_t)M * N4);
       CK(hipMemcpy(xg.data(), dx.p(), M * d * 4, hipMemcpyDeviceToHost));
       CK(hipMemcpy(og.data(), dout.p(), (size_t)M * N4 * 2, hipMemcpyDeviceToHost));
-      double ex = 0, eo = 0, mo = 0, ex1 = 0, est = 0, xchg = 0;
+      double ex = 0, eo = 0, mo = 0, ex1 = 0, est = 0, est2 = 0, xchg = 0;
       for (int i = 0; i < M * d; ++i) xchg = std::max(xchg, (double)std::fabs(xg[i] - x1[i]));
       for (int t = 0; t < d / 16; ++t)
         for (int r = 0; r < M; ++r) {
-          double s1 = 0;
+          double s1 = 0, m2 = 0;
           for (int c = 16 * t; c < 16 * t + 16; ++c) s1 += x1[r * d + c];
-          est = std::max(est, std::fabs(s1 - st1[(t * M + r) * 2]));
+          for (int c = 16 * t; c < 16 * t + 16; ++c) m2 += (x1[r * d + c] - s1 / 16) * (x1[r * d + c] - s1 / 16);
+          est = std::max(est, std::fabs(s1 - st1[(t * M + r) * 2]) / (std::fabs(s1) + 1.0));
+          est2 = std::max(est2, std::fabs(m2 - st1[(t * M + r) * 2 + 1]) / (m2 + 1e-3));
         }
       for (int r = 0; r < M; ++r) {
         std::vector<double> xn(d);
@@ -164,11 +169,12 @@ int main() {
       }
       int dmg = 0;
       for (const Guarded* gg : {&dx, &dbias, &dg, &db, &dao, &dW, &dW1, &dst, &dout, &dws}) dmg += guard_damage(*gg);
-      const bool ok = ex < 1e-3 && eo < 0.02 * mo + 1e-3 && dmg == 0;
+      // residual: f32 sums of |x| up to ~1000 (ulp 6e-5); stats: relative; LN output: bf16 operands (0.4 % each)
+      const bool ok = ex < 1e-3 * (1.0 + offset / 10) && est < 1e-5 && est2 < 1e-3 && eo < 0.01 * mo + 1e-3 && dmg == 0;
       fails += !ok;
-      std::printf("d=%4d M=%2d  residual max err %.2e (after the producer alone %.2e; changed by the consumer %.2e; "
-                  "row-sum stats err %.2e)  output max err %.2e (max |out| %.2f)  guard bytes changed %d  %s\n", d, M, ex, ex1,
-                  xchg, est, eo, mo, dmg, ok ? "ok" : "FAIL");
+      std::printf("offset %6.0f d=%4d M=%2d  residual max err %.2e (after the producer alone %.2e; changed by the consumer "
+                  "%.2e; tile sum rel err %.2e, tile M2 rel err %.2e)  output max err %.2e (max |out| %.2f)  guard bytes "
+                  "changed %d  %s\n", offset, d, M, ex, ex1, xchg, est, est2, eo, mo, dmg, ok ? "ok" : "FAIL");
       for (Guarded* gg : {&dx, &dbias, &dg, &db, &dao, &dW, &dW1, &dst, &dout, &dws}) CK(hipFree(gg->base));
     }
   std::printf("%s\n", fails ? "FAILURES" : "all ok");

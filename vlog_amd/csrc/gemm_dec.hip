@@ -597,8 +597,10 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
       }
   } else {
     // LayerNorm-consuming operand (MF == 1: M <= 16).  Issued together with the weight stream: this wave's f32
-    // activation chunks, the block's affine range (into LDS) and the producer's partial row sums; then
-    // A = bf16((x - mean) * rstd * g + b), the arithmetic of resid_ln_reduce_kernel's output.
+    // activation chunks, the block's affine range (into LDS) and the producer's per-tile row statistics (sum and
+    // sum of squares about the tile's own mean); then A = bf16((x - mean) * rstd * g + b).  The variance is
+    // two-pass-equivalent: within-tile M2 plus 16 (tile mean - mean)^2 per tile, after the mean (no E[x^2] - mean^2
+    // cancellation), so it agrees with resid_ln_reduce_kernel's two-pass statistics to f32 rounding.
     __shared__ __attribute__((aligned(16))) float sg[1280], sb[1280];
     const int m = min(lane & 15, M - 1);
     const float* xr = a.lnx + (long long)m * a.ld + kb + 8 * (lane >> 4);
@@ -628,12 +630,11 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
       bv[j] = a.ln_b[kb + i];
     }
     {
-      float q1 = 0.f, q2 = 0.f;
+      float q1 = 0.f;
 #pragma unroll
       for (int j = 0; j < TG; ++j)
-        if (t0 + j < t1) { q1 += sv[j].x; q2 += sv[j].y; }
+        if (t0 + j < t1) q1 += sv[j].x;
       sst[g][r16][0] = q1;
-      sst[g][r16][1] = q2;
     }
 #pragma unroll
     for (int j = 0; j < 5; ++j)
@@ -642,15 +643,26 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
         sb[tid + 256 * j] = bv[j];
       }
     __syncthreads();
-    float p1 = 0.f, p2 = 0.f;
+    float p1 = 0.f;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      p1 += sst[g][lane & 15][0];
-      p2 += sst[g][lane & 15][1];
-    }
+    for (int g2 = 0; g2 < 16; ++g2) p1 += sst[g2][lane & 15][0];
     const float invn = 1.0f / (float)(a.ln_tiles * 16);
-    const float mean = p1 * invn;
-    const float rstd = rsqrtf(fmaxf(p2 * invn - mean * mean, 0.f) + 1e-5f);
+    const float mean = p1 * invn;                            // row lane & 15 == row tid & 15 (this thread's tiles)
+    {
+      float q2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < TG; ++j)
+        if (t0 + j < t1) {
+          const float dm = sv[j].x * (1.0f / 16.0f) - mean;
+          q2 += sv[j].y + 16.0f * dm * dm;
+        }
+      sst[g][r16][1] = q2;
+    }
+    __syncthreads();
+    float p2 = 0.f;
+#pragma unroll
+    for (int g2 = 0; g2 < 16; ++g2) p2 += sst[g2][lane & 15][1];
+    const float rstd = rsqrtf(p2 * invn + 1e-5f);
 #pragma unroll
     for (int s = 0; s < KSW; ++s)
       if (s0 + s < s1) {
@@ -682,25 +694,32 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
   const int col0 = n0 + 4 * (lane >> 4);
   if (KIND == EPI_RESID_F32 && epi.stat_out) {
     // residual producer for a LayerNorm-consuming GEMM (no split-K): x += acc + bias in place, and this tile's
-    // partial row sums of the new x (columns summed in a fixed order: the 4 of a lane, then the 4 lanes)
+    // row statistics of the new x: the sum, then the sum of squares about the tile mean (columns in a fixed order:
+    // the 4 of a lane, then the 4 lanes)
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       const f32x4 v = sred[0][i][lane] + sred[1][i][lane] + sred[2][i][lane] + sred[3][i][lane];
       const int row = i * 16 + (lane & 15);
       const bool ok = row < M && col0 < N;
       float q1 = 0.f, q2 = 0.f;
+      f32x4 xs = f32x4{0.f, 0.f, 0.f, 0.f};
       if (ok) {
         f32x4 u = v;
         if (epi.bias) u += *(const f32x4*)(epi.bias + col0);
         f32x4* xp = (f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0);
         const f32x4 xn = *xp + u;
         *xp = xn;
+        xs = xn;
         q1 = (xn[0] + xn[1]) + (xn[2] + xn[3]);
-        q2 = (xn[0] * xn[0] + xn[1] * xn[1]) + (xn[2] * xn[2] + xn[3] * xn[3]);
       }
       q1 += __shfl_xor(q1, 16, 64);
-      q2 += __shfl_xor(q2, 16, 64);
       q1 += __shfl_xor(q1, 32, 64);
+      if (ok) {
+        const float mt = q1 * (1.0f / 16.0f);
+        const float d0 = xs[0] - mt, d1 = xs[1] - mt, d2 = xs[2] - mt, d3 = xs[3] - mt;
+        q2 = (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+      q2 += __shfl_xor(q2, 16, 64);
       q2 += __shfl_xor(q2, 32, 64);
       if (ok && lane < 16) *(float2*)(epi.stat_out + ((long long)tile * M + row) * 2) = make_float2(q1, q2);
     }
