@@ -441,7 +441,13 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     host_group = None
+    json_fd = None
     if world > 1:
+        # the process-group backends print connection notices on stdout ("[Gloo] Rank ..."); the driver reads ONE
+        # JSON line from rank 0, so fd 1 goes to stderr for the run and the line is written to the saved stdout
+        sys.stdout.flush()
+        json_fd = os.dup(1)
+        os.dup2(2, 1)
         import torch.distributed as dist
         backend = os.environ.get("VLOG_AMD_BENCH_BACKEND", "nccl")
         if backend == "nccl":
@@ -650,7 +656,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline(dims, sd, mean_tok)
         except Exception as e:  # reported, never fatal to the GPU measurement
             out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
-    print(json.dumps(out), flush=True)
+    if json_fd is not None:
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    else:
+        print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
