@@ -266,6 +266,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "cross_tf" (default 1): the teacher-forced passes of wm_align / wm_align_batch (projected form) run the
  *   cross-attention on the matrix cores (bf16 MFMA, f32 scores and captured probabilities; the attention weights
  *   enter the V product as bf16); 0 = the f32 VALU kernels of the decode path.
+ *   "cross_mfma" (default 1): projected form, decode passes whose windows have 2..32 rows (beam hypotheses, prompt
+ *   prefill) run the cross-attention on the same matrix-core kernel, the keys split over blocks to fill the chip and
+ *   merged by the split-combine kernel; 0 = the f32 VALU group kernel.  Changes numerics at bf16-rounding level.
  *   "debug_nan_row" (default -1, TEST ONLY): >= 0 overwrites logits row r of every decode pass of wm_generate with
  *   NaN before token selection (exercises the failure contract of wm_generate). */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);

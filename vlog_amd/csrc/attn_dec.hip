@@ -754,18 +754,23 @@ typedef __attribute__((ext_vector_type(2))) int tf_i32x2;
 __device__ __forceinline__ int tf_kslot(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 7)) << 3); }
 __device__ __forceinline__ int tf_vslot(int r, int c) { return r * 64 + ((c ^ (((r >> 1) & 1) << 2)) << 3); }
 
+// Key splits (a.splits > 1, no capture): block (window, head, row tile, split) takes tiles [split nt / S, (split+1) nt / S)
+// and writes its (m, l, unnormalised o) partial for cross_combine_kernel, as the VALU kernels do.  This is also the
+// decode path of beam groups (`group` = the window's hypotheses, 2..32 rows padded to one 32-row wave tile).
 __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int group, int nqt) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TF_KT * HD];     // [buf][K | V][64 keys][64]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ql = lane & 31, hh = lane >> 5;
   const int H = a.H, T = a.T;
-  int qt, h, g;
+  int qt, h, g, sp;
   {
     // XCD-aware: the row tiles of one (window, head) get consecutive remapped ids (one XCD's L2 holds the panels)
     const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     qt = wgid % nqt;
-    const int rest = wgid / nqt;
+    int rest = wgid / nqt;
+    sp = rest % a.splits;
+    rest /= a.splits;
     h = rest % H;
     g = rest / H;
   }
@@ -784,19 +789,41 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
     atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), (unsigned long long)((cap ? 3 : 2) * T * HD * 2));
   const int r = qt * 128 + wv * 32 + ql;
   const bool valid = r < group;
+  const bool wave_on = qt * 128 + wv * 32 < group;     // wave-uniform: a wave with no row only stages tiles
   bf16x8 qf[4];
-  {
+  if (a.q_part) {
+    // q = bf16(sum of the cq split-K slabs in slab order + bias), as splitk_reduce_kernel forms it (bit-identical
+    // to the unfused bf16 q); every slab load of the lane is issued before the adds
+    const long long slab = (long long)a.q_rows * a.ldq;
+    const float* qp = a.q_part + (long long)(row0 + min(r, group - 1)) * a.ldq + h * HD + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+      for (int k = 0; k < a.q_splits; ++k) {
+        v0 += *(const f32x4*)(qp + k * slab + 16 * s);
+        v1 += *(const f32x4*)(qp + k * slab + 16 * s + 4);
+      }
+      const float* bq = a.q_bias + h * HD + 8 * hh + 16 * s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        qf[s][j] = f2bf(v0[j] + bq[j]);
+        qf[s][4 + j] = f2bf(v1[j] + bq[4 + j]);
+      }
+    }
+  } else {
     const bf16* qp = a.q + (long long)(row0 + min(r, group - 1)) * a.ldq + h * HD + 8 * hh;
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
   }
   const float sl2 = a.scale_log2;
-  const int nt = (T + TF_KT - 1) / TF_KT;
+  const int ntt = (T + TF_KT - 1) / TF_KT;
+  const int tb = sp * ntt / a.splits, te = (sp + 1) * ntt / a.splits;   // this split's key tiles
+  const int nt = te - tb;
   i32x4 rk[2], rv[2];
   auto load_tile = [&](int t, bool withv) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int c = tid + i * 256, key = min(t * TF_KT + (c >> 3), T - 1), ch = c & 7;
+      const int c = tid + i * 256, key = min((tb + t) * TF_KT + (c >> 3), T - 1), ch = c & 7;
       rk[i] = __builtin_nontemporal_load((const i32x4*)(K + (long long)key * HD + ch * 8));
       if (withv) rv[i] = __builtin_nontemporal_load((const i32x4*)(V + (long long)key * HD + ch * 8));
     }
@@ -824,7 +851,7 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int key = t * TF_KT + kb * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
+        const int key = (tb + t) * TF_KT + kb * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
         sc[kb][e] = key < T ? sc[kb][e] * sl2 : -INFINITY;
       }
     }
@@ -839,20 +866,22 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
     for (int t = 0; t < nt; ++t) {
       const bf16* sK = smem + (t & 1) * (2 * TF_KT * HD);
       if (t + 1 < nt) load_tile(t + 1, false);
-      f32x16 sc[2];
-      scores(sK, t, sc);
-      float mx = m_run;
+      if (wave_on) {
+        f32x16 sc[2];
+        scores(sK, t, sc);
+        float mx = m_run;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sc[kb][e]);
-      float acc = 0.f;
+          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sc[kb][e]);
+        float acc = 0.f;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc += exp2f(sc[kb][e] - mx);
-      l_run = l_run * exp2f(m_run - mx) + acc;     // mx is finite: every tile holds a key < T
-      m_run = mx;
+          for (int e = 0; e < 16; ++e) acc += exp2f(sc[kb][e] - mx);
+        l_run = l_run * exp2f(m_run - mx) + acc;   // mx is finite: every tile holds a key < T
+        m_run = mx;
+      }
       if (t + 1 < nt) store_tile((t + 1) & 1, false);
       __syncthreads();
     }
@@ -877,6 +906,7 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
     const bf16* sK = smem + (t & 1) * (2 * TF_KT * HD);
     const bf16* sV = sK + TF_KT * HD;
     if (t + 1 < nt) load_tile(t + 1, true);
+    if (wave_on) {
     f32x16 sc[2];
     scores(sK, t, sc);
     if (!cap) {
@@ -910,7 +940,7 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
       if (prow) {
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
-          const int key = t * TF_KT + kb * 32 + 8 * gg + 4 * hh;
+          const int key = (tb + t) * TF_KT + kb * 32 + 8 * gg + 4 * hh;
           if (key < T)
             *(f32x4*)(prow + key) = f32x4{pv[4 * gg] * inv_cap, pv[4 * gg + 1] * inv_cap, pv[4 * gg + 2] * inv_cap,
                                           pv[4 * gg + 3] * inv_cap};
@@ -936,10 +966,26 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
           const bf16x8 va = __builtin_bit_cast(bf16x8, i32x4{vw[0][0], vw[0][1], vw[1][0], vw[1][1]});
           o[hb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[kb][s], o[hb], 0, 0, 0);
         }
+    }
     if (t + 1 < nt) store_tile((t + 1) & 1, true);
     __syncthreads();
   }
   if (!cap) l_run += __shfl_xor(l_run, 32, 64);
+  if (valid && a.splits > 1) {
+    // partial of this key split (unnormalised o, its max and sum in log2 units) for cross_combine_kernel
+    const long long pi = ((long long)(row0 + r) * H + h) * a.splits + sp;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+        *(f32x4*)(a.part_o + pi * HD + 32 * hb + 8 * gg + 4 * hh) =
+            f32x4{o[hb][4 * gg], o[hb][4 * gg + 1], o[hb][4 * gg + 2], o[hb][4 * gg + 3]};
+    if (hh == 0) {
+      a.part_m[pi] = m_run;
+      a.part_l[pi] = l_run;
+    }
+    return;
+  }
   if (valid) {
     const float inv = cap ? inv_cap : 1.0f / l_run;
     bf16* orow = a.out + (long long)(row0 + r) * a.ldo + h * HD;
@@ -1004,15 +1050,38 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
   a.out = out; a.ldo = ldo; a.H = H; a.T = T; a.n_ctx = T;
   a.part_m = part_m; a.part_l = part_l; a.part_o = part_o; a.probs = probs; a.head_map = head_map; a.n_align = n_align;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;
-  if (fz.tf && group >= 16 && rows % group == 0 && !fz.q_part) {
+  // matrix-core form: teacher-forced passes (>= 16 rows per window), and with fz.mfma the decode passes of row groups
+  // (beam hypotheses / prefill rows of a window; 2..32 rows)
+  const bool mf_tf = fz.tf && group >= 16;
+  const bool mf_dec = !fz.tf && fz.mfma && group >= 2 && group <= 32 && !probs;
+  if ((mf_tf || mf_dec) && rows % group == 0) {
     if (probs && !head_map) throw std::runtime_error("cross_attn: capture without a head map");
-    a.splits = 1;
     const int nqt = (group + 127) / 128;
-    const long long nblk = (long long)(rows / group) * H * nqt;
+    const int ntt = (T + 63) / 64;
+    int splits = 1;
+    if (mf_dec) {
+      // key splits until ~2 rounds of blocks fill the chip; a function of the whole pass (plan_rows), so a row's
+      // summation order does not depend on how the pass is sliced
+      const int plan_blocks = plan_rows / group * H * nqt;
+      splits = std::max(1, std::min(std::min(16, ntt), (512 + plan_blocks - 1) / plan_blocks));
+    }
+    a.splits = splits;
+    const long long nblk = (long long)(rows / group) * H * nqt * splits;
     if (nblk > (1LL << 31) - 1) throw std::runtime_error("cross_attn: grid too large");
-    if (ev0) hipExtLaunchKernelGGL(cross_tf_kernel, dim3((unsigned)nblk), dim3(256), 0, st, ev0, ev1, 0, a, group, nqt);
+    if (splits > 1 && (!part_m || !part_l || !part_o)) throw std::runtime_error("cross_attn: no split scratch");
+    hipEvent_t e1 = splits == 1 ? ev1 : nullptr;
+    if (ev0) hipExtLaunchKernelGGL(cross_tf_kernel, dim3((unsigned)nblk), dim3(256), 0, st, ev0, e1, 0, a, group, nqt);
     else hipLaunchKernelGGL(cross_tf_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a, group, nqt);
     WM_LAUNCH_CHECK("cross_tf_kernel");
+    if (splits > 1) {
+      if (ev1)
+        hipExtLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, nullptr, ev1, 0, part_m, part_l,
+                              part_o, row_hyp, done, out, ldo, H, splits);
+      else
+        hipLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, part_m, part_l, part_o, row_hyp, done,
+                           out, ldo, H, splits);
+      WM_LAUNCH_CHECK("cross_combine_kernel");
+    }
     return;
   }
   if (!hyp_slot) throw std::runtime_error("cross_attn: no slot table outside the teacher-forced kernel");

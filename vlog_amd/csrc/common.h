@@ -61,6 +61,7 @@ struct CrossFuse {
   const float* q_bias = nullptr;
   int* cnt = nullptr;              // >= rows*H zeroed ints (nullptr: separate combine kernel)
   int tf = 0;                      // teacher-forced pass (`group` contiguous rows per window): matrix-core kernel
+  int mfma = 0;                    // decode pass: row groups of 2..32 rows per window on the matrix-core kernel
 };
 
 // Launch check used by every host-side launcher: converts an asynchronous launch failure into an

@@ -194,6 +194,7 @@ struct wm_engine {
   // per large-v3 window, projected by wm_cross_kv)
   int cross_mode = 1;
   int cross_tf = 1;          // teacher-forced passes (alignment) run the projected form's cross-attention on MFMA
+  int cross_mfma = 1;        // projected form, decode passes with 2..32 rows per window (beam groups): MFMA kernel
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
                              // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
@@ -604,6 +605,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   }
   if ((e->cross_fuse & 2) && e->cross_mode == 0) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   fz.tf = (attn && align_map && e->cross_tf) ? 1 : 0;
+  fz.mfma = e->cross_mfma;
   float* probs = nullptr;
   const int* hmap = nullptr;
   if (attn && align_map) {
@@ -2150,6 +2152,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     }
     else if (k == "debug_nan_row") e->dbg_nan_row = (int)std::max<int64_t>(-1, std::min<int64_t>(value, 1 << 30));
     else if (k == "cross_tf") e->cross_tf = value ? 1 : 0;
+    else if (k == "cross_mfma") e->cross_mfma = value ? 1 : 0;
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }
@@ -2189,6 +2192,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_mode") *value = e->cross_mode;
     else if (k == "debug_nan_row") *value = e->dbg_nan_row;
     else if (k == "cross_tf") *value = e->cross_tf;
+    else if (k == "cross_mfma") *value = e->cross_mfma;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
   });
 }
