@@ -406,7 +406,7 @@ def main():
                          "model; same kernels and token counts, but near-tied logits (the parity gates cannot hold)")
     ap.add_argument("--check-every", type=int, default=4, help="decode steps between host polls of the live count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: profiles/traffic_r03_c.json, "
+    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: profiles/traffic_r04_a.json, "
                     "or traffic_r02_fp8.json with --cross-fp8)")
     ap.add_argument("--cross-fp8", action="store_true", help="opt-in fp8 (e4m3) cross memory: not the headline")
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-kernel event timing")
@@ -430,7 +430,7 @@ def main():
     if args.balance is None:
         args.balance = "tokens" if args.workload == "variable" else "count"
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r03_c.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r04_a.json")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
