@@ -430,7 +430,10 @@ def main():
     if args.balance is None:
         args.balance = "tokens" if args.workload == "variable" else "count"
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r04_a.json")
+        # the committed PMC files were measured on the default workload (uniform greedy, 150 windows); another
+        # workload's launches move other bytes, so its line carries traffic null unless a file is given
+        args.traffic_json = (os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r04_a.json")
+                             if args.beam == 1 and args.workload == "uniform" and args.windows == 150 else "")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
