@@ -667,6 +667,9 @@ class BatchedInferencePipeline:
     def __init__(self, model: WhisperModel, max_batch_windows: int = 150):
         self.model = model
         self.max_batch_windows = max_batch_windows
+        # finished windows leave the decode passes (greedy: the row-set decode's compaction; beam: finished windows'
+        # hypotheses); VLOG_AMD_COMPACT=0 keeps every row to the batch's end
+        self.compact = os.environ.get("VLOG_AMD_COMPACT", "1") != "0"
 
     # -- windows of the whole-file feature matrix
     @staticmethod
@@ -759,7 +762,7 @@ class BatchedInferencePipeline:
                         temperature=T, num_hypotheses=options.best_of if sampling else 1, seed=seed + 7919 * ti + b0,
                         suppress_tokens=options.suppress_tokens, suppress_blank=options.suppress_blank,
                         max_initial_timestamp_index=mit, with_timestamps=not options.without_timestamps,
-                        sot_index=prompt.index(st.sot), check_every=4, compact=True)
+                        sot_index=prompt.index(st.sot), check_every=4, compact=self.compact)
                     still = []
                     for i, r in zip(pending, res):
                         alp = segs.avg_logprob(r.score, len(r.tokens), options.length_penalty)
