@@ -61,6 +61,19 @@ __device__ __forceinline__ f32x16 xzero16() {
 // over the 16 rows of a lane group (rows of equal r mod 4 differ in (r >> 2) & 3 inside every group of the
 // b128 lane-group table), and ds_read_b64_tr_b16 of 4 rows (4k..4k+3) x 64 B (slots 4i + quad).
 __device__ __forceinline__ int xchunk(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+// The cross-wave S reduction's barrier.  RAW: the LDS writes before it are retired by lgkmcnt(0).  With LDS-DMA in
+// flight (the split-staging form) __syncthreads would also drain vmcnt (the compiler orders the pending DMA's LDS
+// writes before a workgroup fence), i.e. wait for the next tiles' loads at every barrier; the wave-private DMA
+// images are ordered for their own wave by the counted vmcnt at each tile instead (MI355X_MICROARCH.md item 7).
+template <bool RAW>
+__device__ __forceinline__ void xbarrier() {
+  if constexpr (RAW) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else {
+    __syncthreads();
+  }
+}
 __host__ __device__ constexpr int xldr(int qw) { return (qw / 8 + ((4 - qw / 8) % 16 + 16) % 16) * 8; }
 
 // ------------------------------------------------------------------------------------------------------
@@ -231,8 +244,13 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   constexpr int EB = F8 ? 1 : 2;                         // bytes per stored E element
   const char* E = (const char*)a.enc + ((long long)slot * a.T * a.d + cb) * EB;
   const float* Es = F8 ? a.escale + (long long)slot * a.T : nullptr;
-  bf16* sE = (bf16*)smem + wv * 32 * LDR;
-  float* sX = (float*)(smem + NW * 32 * LDR * 2);        // [NW][16][64] S^T partials
+  // DEPTH 3 (split staging): per wave, rows 0-15 of a tile land by LDS-DMA in one of two 16-row images (one tile
+  // ahead) and rows 16-31 come through registers two tiles ahead into a third 16-row image: 15 KB of E in flight per
+  // wave instead of 10 KB, at the same 40 staging VGPRs.  Otherwise one 32-row image per wave.
+  constexpr int IMGR = DEPTH == 3 ? 48 : 32;              // image rows per wave
+  bf16* sE = (bf16*)smem + wv * IMGR * LDR;
+  bf16* sER = DEPTH == 3 ? sE + 32 * LDR : sE + 16 * LDR; // rows 16-31 (DEPTH 3: the register-fed image)
+  float* sX = (float*)(smem + NW * IMGR * LDR * 2);      // [NW][16][64] S^T partials
   float* sRed = sX + NW * 16 * 64;                       // [16][64] their sums
   {
     const unsigned long long nq = __popcll(__ballot(valid && hh == 0));
@@ -277,7 +295,38 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     if (F8) scl = Es[min(tile * 32 + (lo & 31), a.T - 1)];
   };
   float* sScale = nullptr;
-  if (F8) sScale = (float*)(smem + NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4) + wv * 32;
+  if (F8) sScale = (float*)(smem + NW * IMGR * LDR * 2 + (NW + 1) * 16 * 64 * 4) + wv * 32;
+  // DEPTH 3 loads.  Rows 16-31 of a tile: LS / 2 16-B loads per lane into a register half-set; rows 0-15: LS / 2
+  // LDS-DMA wave-instructions of 1 KiB each, lane-linear in the 16-row image, so each lane fetches the chunk that
+  // the image's swizzle puts at its destination slot (c = slot ^ ((row >> 2) & 3), the inverse of xchunk).
+  constexpr int LH = LS / 2;
+  auto load_hi = [&](i32x4 (&stg)[LH], int tile, int lo) {
+#pragma unroll
+    for (int i = 0; i < LH; ++i) {
+      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
+      const int t = min(tile * 32 + 16 + r, a.T - 1);
+      stg[i] = __builtin_nontemporal_load((const i32x4*)(E + ((long long)t * a.d) * EB + ch * 16));
+    }
+  };
+  auto store_hi = [&](const i32x4 (&stg)[LH], int lo) {
+#pragma unroll
+    for (int i = 0; i < LH; ++i) {
+      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
+      *(i32x4*)(sER + r * LDR + 8 * xchunk(r, ch)) = stg[i];
+    }
+  };
+  auto dma_lo = [&](int tile, int buf, int lo) {
+    bf16* img = sE + buf * 16 * LDR;
+#pragma unroll
+    for (int i = 0; i < LH; ++i) {
+      const int pb = i * 1024 + 16 * lo;                 // byte offset of this lane's 16 B in the image
+      const int r = pb / (LDR * 2), sl = (pb - r * LDR * 2) >> 4;
+      const int c = sl ^ ((r >> 2) & 3);
+      const int t = min(tile * 32 + r, a.T - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(E + ((long long)t * a.d) * EB + c * 16),
+                                       (__attribute__((address_space(3))) void*)(img + i * 512), 16, 0, 2);
+    }
+  };
   float* pr_row = nullptr;
   if (a.probs && wv == 0 && valid) {
     const int hm = a.head_map[hd];
@@ -285,9 +334,17 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   }
   // one tile: its staged registers -> the wave's LDS image, the loads of tile + DEPTH into the same
   // registers, then S^T, the cross-wave sum, the online softmax and U^T
-  auto tile_step = [&](int tile, i32x4 (&stg)[LS], float& scl) {
+  auto tile_step = [&](int tile, auto& stg, float& scl, int buf) {
     int lo = lane;
     asm volatile("" : "+v"(lo));
+    bf16* sEA = DEPTH == 3 ? sE + buf * 16 * LDR : sE;    // rows 0-15 of this tile
+    if constexpr (DEPTH == 3) {
+      // this tile's rows 16-31 (registers) to their image, then the loads two tiles ahead into the same registers
+      // and the DMA of the next tile's rows 0-15; rows 0-15 of THIS tile were retired by the caller's vmcnt
+      store_hi(stg, lo);
+      if (tile + 1 < te) dma_lo(tile + 1, buf ^ 1, lo);
+      if (tile + 2 < te) load_hi(stg, tile + 2, lo);
+    } else {
     // wave-private LDS image of this tile (this wave's earlier reads of it are complete: LDS is in order);
     // F8: each 16-B chunk of 16 e4m3 values becomes two bf16 chunks (exact: e4m3 is a subset of bf16)
     int r = lo / CPR, ch = lo % CPR;     // chunk (r, ch) of load i, stepped like the global offsets
@@ -318,13 +375,15 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     }
     if (F8 && lo < 32) sScale[lo] = scl;
     if (tile + DEPTH < te) load(stg, scl, tile + DEPTH, lo);
+    }
     // ---- S^T partial over this wave's columns
     f32x16 sc = xzero16();
     {
       // A fragment of k-step s: row l32, chunk 2s + hh -> stored at 4 (s >> 1) + ((2 (s & 1) + hh) ^ g)
       const int l32o = lo & 31, g = (l32o >> 2) & 3;
-      const bf16* s0 = sE + l32o * LDR + 8 * (hh ^ g);
-      const bf16* s1 = sE + l32o * LDR + 8 * ((2 + hh) ^ g);
+      const bf16* rb = l32o < 16 ? sEA + l32o * LDR : sER + (l32o - 16) * LDR;
+      const bf16* s0 = rb + 8 * (hh ^ g);
+      const bf16* s1 = rb + 8 * ((2 + hh) ^ g);
       if (!(ABL & 1)) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -338,7 +397,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     if (!(ABL & 2)) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sX[(wv * 16 + r) * 64 + lane] = sc[r];
-      __syncthreads();
+      xbarrier<DEPTH == 3>();
       // wave w sums registers r = w, w + NW, ... over the waves in order 0..NW-1 (any NW)
 #pragma unroll
       for (int k = 0; k < (16 + NW - 1) / NW; ++k) {
@@ -349,7 +408,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
         for (int w2 = 1; w2 < NW; ++w2) v += sX[(w2 * 16 + r) * 64 + lane];
         sRed[r * 64 + lane] = v;
       }
-      __syncthreads();
+      xbarrier<DEPTH == 3>();
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc[r] = sRed[r * 64 + lane];
     }
@@ -406,13 +465,43 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     if (!(ABL & 4)) {
       const int G4 = (lo >> 4) & 3, gi = lo & 15, gq = gi >> 2, gp = gi & 3;
       const int lowc = 2 * (G4 & 1) + (gp >> 1);
-      const bf16* tb0 = sE + (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
-      const bf16* tb1 = sE + (8 + 4 * hh + gq) * LDR + 8 * (lowc ^ (2 + hh)) + 4 * (gp & 1);
+      const int o0 = (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
+      const int o1 = (8 + 4 * hh + gq) * LDR + 8 * (lowc ^ (2 + hh)) + 4 * (gp & 1);
+      if constexpr (DEPTH == 3) {
+        // transposed reads as inline asm: the compiler gives the tr16 intrinsic no alias information and would
+        // drain vmcnt (the next tiles' DMA and loads) before it; this tile's images were retired by the tile's
+        // vmcnt, and the DMA in flight writes the other buffer.  Each c's four reads, then their lgkmcnt.
+        auto lds_addr = [](const bf16* p) -> unsigned {
+          return (unsigned)(size_t)(__attribute__((address_space(3))) const bf16*)p;
+        };
+        const unsigned a00 = lds_addr(sEA + o0), a01 = lds_addr(sEA + o1);
+        const unsigned a10 = lds_addr(sER + o0), a11 = lds_addr(sER + o1);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          xi32x2 r00, r01, r10, r11;
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %4 offset:%8\n\t"
+              "ds_read_b64_tr_b16 %1, %5 offset:%8\n\t"
+              "ds_read_b64_tr_b16 %2, %6 offset:%8\n\t"
+              "ds_read_b64_tr_b16 %3, %7 offset:%8\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=v"(r00), "=v"(r01), "=v"(r10), "=v"(r11)
+              : "v"(a00), "v"(a01), "v"(a10), "v"(a11), "i"(64 * c)
+              : "memory");
+          const bf16x8 va0 = __builtin_bit_cast(bf16x8, i32x4{r00[0], r00[1], r01[0], r01[1]});
+          const bf16x8 va1 = __builtin_bit_cast(bf16x8, i32x4{r10[0], r10[1], r11[0], r11[1]});
+          o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, pf[0], o[c], 0, 0, 0);
+          o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, pf[1], o[c], 0, 0, 0);
+        }
+      } else
 #pragma unroll
       for (int c = 0; c < CT; ++c)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          const int off = 16 * ks * LDR + 32 * c;
+          // rows 16 ks .. 16 ks + 15: image of rows 0-15 or of rows 16-31 (same swizzle: (r >> 2) & 3 repeats)
+          const bf16* tb0 = (ks ? sER : sEA) + o0;
+          const bf16* tb1 = (ks ? sER : sEA) + o1;
+          const int off = 32 * c;
           const xi32x2 v0 = __builtin_bit_cast(xi32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                                                             (__attribute__((address_space(3))) xi16x4*)(tb0 + off)));
           const xi32x2 v1 = __builtin_bit_cast(xi32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -422,11 +511,32 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
         }
     }
   };
-  if (tb < te) load(stgA, scA, tb, lane);
-  if (DEPTH == 2 && tb + 1 < te) load(stgB, scB, tb + 1, lane);
-  for (int tile = tb; tile < te; tile += DEPTH) {
-    tile_step(tile, stgA, scA);
-    if (DEPTH == 2 && tile + 1 < te) tile_step(tile + 1, stgB, scB);
+  if constexpr (DEPTH == 3) {
+    // issue order R(tb), DMA(tb), R(tb+1); at each tile the loads younger than its own are the next tile's
+    // register half (LH), so vmcnt(LH) retires this tile's DMA and registers (the last tile: vmcnt(0))
+    i32x4 h0[LH], h1[LH];
+    if (tb < te) {
+      load_hi(h0, tb, lane);
+      dma_lo(tb, 0, lane);
+    }
+    if (tb + 1 < te) load_hi(h1, tb + 1, lane);
+    for (int tile = tb; tile < te; tile += 2) {
+      if (tile + 1 < te) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(LH) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tile_step(tile, h0, scA, 0);
+      if (tile + 1 < te) {
+        if (tile + 2 < te) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(LH) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tile_step(tile + 1, h1, scA, 1);
+      }
+    }
+  } else {
+    if (tb < te) load(stgA, scA, tb, lane);
+    if (DEPTH == 2 && tb + 1 < te) load(stgB, scB, tb + 1, lane);
+    for (int tile = tb; tile < te; tile += DEPTH) {
+      tile_step(tile, stgA, scA, 0);
+      if (DEPTH == 2 && tile + 1 < te) tile_step(tile + 1, stgB, scB, 0);
+    }
   }
   l_run += __shfl_xor(l_run, 32, 64);
   if (valid) {
@@ -456,7 +566,8 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
 template <int QW, int NW, int DEPTH, bool F8 = false, int ABL = 0, bool CAP = false>
 __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   constexpr int LDR = xldr(QW);
-  __shared__ __attribute__((aligned(16))) char smem[NW * 32 * LDR * 2 + (NW + 1) * 16 * 64 * 4 + (F8 ? NW * 32 * 4 : 0)];
+  constexpr int IMGR = DEPTH == 3 ? 48 : 32;
+  __shared__ __attribute__((aligned(16))) char smem[NW * IMGR * LDR * 2 + (NW + 1) * 16 * 64 * 4 + (F8 ? NW * 32 * 4 : 0)];
   const int n_tiles = (a.T + 31) / 32;
   // XCD-aware item order: the blocks of one (group, split), i.e. its m-tiles, run on one XCD at about the
   // same time, so the 2nd..n-th reads of an E tile hit that XCD's L2
@@ -765,6 +876,7 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
     case 1024: if (form) { XA_LAUNCH(256, 4, 2); } else { XA_LAUNCH(128, 8, 1); } break;
     case 1280:
       if (form == 2) { XA_LAUNCH(128, 10, 2); }          // 10 waves x 128 columns, two tiles staged ahead
+      else if (form == 3) { XA_LAUNCH(160, 8, 3); }      // split staging: rows 0-15 by LDS-DMA, 16-31 two ahead
       else if (form) { XA_LAUNCH(320, 4, 2); }
       else { XA_LAUNCH(160, 8, 1); }
       break;
