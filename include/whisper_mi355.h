@@ -247,6 +247,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_gemm_cols.<proj>" (preset 1: 64 for fc1 and fc2, else 32): output columns per ring-GEMM block, 32 or 64 (64
  *   takes row groups of at most 64; other routes ignore it).  Bit-identical either way.  decode_gemm_plan also
  *   resets these to its preset.
+ *   "decode_gemm_big_rows" (default 320): passes of at least this many rows (<= 1024; beam groups of many windows)
+ *   route every projection to 64-row ring groups over its whole K (64 columns for qkv / fc1, and for all from 512
+ *   rows; 0 disables).  Results agree to f32 rounding.
  *   "gemm_persistent" (default 0, process-wide): 1 runs large encoder GEMMs as one persistent block per CU
  *   walking its tiles, the next tile's first K-tiles loaded during the current tile's last K-steps and epilogue
  *   (measured no faster than one block per tile).  Bit-identical.

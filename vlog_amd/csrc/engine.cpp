@@ -195,6 +195,8 @@ struct wm_engine {
   int cross_mode = 1;
   int cross_tf = 1;          // teacher-forced passes (alignment) run the projected form's cross-attention on MFMA
   int cross_mfma = 1;        // projected form, decode passes with 2..32 rows per window (beam groups): MFMA kernel
+  int dec_big_rows = 320;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
+                             // whole K per block (decoder_layer)
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
                              // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
@@ -539,11 +541,17 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     // one window's beam (or a handful of rows): the weight-streaming small-M kernel
     if (sl.total_rows <= 32 && e->dec_gemv && launch_dec_gemv(a, w, ldw, rows, N, K, ep, ws, wsb, st)) return;
     if (a.lnx || ep.stat_out) throw std::runtime_error("decoder: fused LayerNorm operand off the small-M path");
-    const int p = plan_of(proj);
+    // passes of >= dec_big_rows rows (beam groups of many windows; tools/dec_gemm_bench at 384 and 750 rows): 64-row
+    // ring groups; 64 columns for qkv and fc1, and for every projection from 512 rows; fc2's whole K per block
+    // (384 rows: 76 vs 86 us per layer for the 150-row plan; 750 rows: 114 vs 159 us)
+    const int tr = sl.total_rows;
+    const bool big = e->dec_big_rows > 0 && tr >= e->dec_big_rows && tr <= 1024;
+    const int p = big ? 64 : plan_of(proj);
+    const int cols = big ? ((tr >= 512 || proj == DEC_QKV || proj == DEC_FC1) ? 64 : 32) : e->dec_cols[proj];
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
-    const int kr = e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 ? K : 1280);
-    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, e->dec_cols[proj])) return;
+    const int kr = e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 || big ? K : 1280);
+    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols)) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
     launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
@@ -2153,6 +2161,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "debug_nan_row") e->dbg_nan_row = (int)std::max<int64_t>(-1, std::min<int64_t>(value, 1 << 30));
     else if (k == "cross_tf") e->cross_tf = value ? 1 : 0;
     else if (k == "cross_mfma") e->cross_mfma = value ? 1 : 0;
+    else if (k == "decode_gemm_big_rows") e->dec_big_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }
@@ -2193,6 +2202,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "debug_nan_row") *value = e->dbg_nan_row;
     else if (k == "cross_tf") *value = e->cross_tf;
     else if (k == "cross_mfma") *value = e->cross_mfma;
+    else if (k == "decode_gemm_big_rows") *value = e->dec_big_rows;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
   });
 }
