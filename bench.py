@@ -180,8 +180,10 @@ class Pipeline:
         encoder output goes to its own window slots (K x W slots), then the windows of all K batches decode with W
         rows in flight, longest-expected first, a finished window's row taking the next window (engine.cpp
         generate_rows) — so a batch's short windows no longer wait for its longest one: the decoder steps follow the
-        total tokens, plus one tail at the end.  A production worker streaming its shard does the same.  Results,
-        segments and the WebVTT are produced for every window of every batch."""
+        total tokens, plus one tail at the end.  A production worker streaming its shard does the same.  Beam search:
+        W windows' groups of `beam` rows in flight (engine.cpp generate_rows_beam); word timestamps: one batched
+        alignment over every window at the end.  Results, segments and the WebVTT are produced for every window of
+        every batch."""
         from vlog_amd.shard import expected_token_order, expected_tokens
         eng, W, d = self.eng, self.W, self.dims
         t0 = time.perf_counter()
@@ -212,19 +214,36 @@ class Pipeline:
         exp = expected_tokens(db, 512, [self.margin_left + CLIP * i for i in range(W)], [CLIP] * W)
         order = expected_token_order(np.tile(exp, K))
         gen_stats = {}
+        # beam search: W windows' groups of `beam` rows in flight (engine.cpp generate_rows_beam)
+        kw = dict(beam_size=self.beam, patience=1.0) if self.beam > 1 else {}
         out, steps = eng.generate(order, [self.prompt] * (K * W), suppress_tokens=self.suppress, max_length=448,
-                                  check_every=self.check_every, max_rows=W, compact=True, stats=gen_stats)
+                                  check_every=self.check_every, max_rows=W * max(1, self.beam), compact=True,
+                                  stats=gen_stats, **kw)
         res = [None] * (K * W)
         for w, r in zip(order, out):
             res[w] = r
         t3 = time.perf_counter()
-        n_seg = vtt_bytes = 0
+        groups = []
         for k in range(K):
-            segs = []
             for w in range(W):
                 off = (self.g0 + w) * 30.0
                 cur, _, _ = split_segments_by_timestamps(res[k * W + w].tokens, d.specials.timestamp_begin, off, 3000,
                                                          30.0, w * 3000)
+                groups.append(cur)
+        t_al = 0.0
+        if self.words:
+            # every window's encoder output is still in its slot (k W + w): one batched alignment over all of them
+            ta = time.perf_counter()
+            idx = [i for i, g in enumerate(groups) if g]
+            if idx:
+                self._add_words([groups[i] for i in idx], self.tok, [3000] * len(idx), "\"'“¿([{-",
+                                "\"'.。,，!！?？:：”)]}、", 0.0, slots=idx)
+            t_al = time.perf_counter() - ta
+        n_seg = vtt_bytes = 0
+        for k in range(K):
+            segs = []
+            for w in range(W):
+                cur = groups[k * W + w]
                 for s_ in cur:
                     text = self.tok.decode(s_["tokens"])
                     if s_["start"] == s_["end"] or not text.strip():
@@ -234,8 +253,8 @@ class Pipeline:
             n_seg += len(segs)
             vtt_bytes += len(vtt)
         t4 = time.perf_counter()
-        for k_, v in (("logmel", t_mel), ("encode", t_enc), ("schedule", 0.0), ("decode", t3 - t2), ("align", 0.0),
-                      ("host", t4 - t3)):
+        for k_, v in (("logmel", t_mel), ("encode", t_enc), ("schedule", 0.0), ("decode", t3 - t2), ("align", t_al),
+                      ("host", t4 - t3 - t_al)):
             self.stage[k_] = self.stage.get(k_, 0.0) + v
         import zlib
         crc = 0

@@ -286,9 +286,26 @@ def test_config5_beam_compaction_variable_length(lv3_var):
                                           suppress_tokens=cfg.sup, max_length=448, check_every=4, compact=compact,
                                           stats=st)
             out[compact] = (res, steps, st)
+        # the beam row-set decode (engine.cpp generate_rows_beam): 20 windows' groups in flight, a finished window's
+        # group taking the next one (windows in reverse order, so long and short ones mix), then compaction
+        order = list(range(W))[::-1]
+        st_rows = {}
+        res_rows, _ = cfg.eng.generate(order, [cfg.prompt] * W, beam_size=5, patience=1.0, suppress_tokens=cfg.sup,
+                                       max_length=448, check_every=4, max_rows=100, compact=True, stats=st_rows)
+        rc = [None] * W
+        for w, r in zip(order, res_rows):
+            rc[w] = r
     finally:
         cfg.eng.set_option("cross_mode", 1)
     (ra, sa, ta), (rb, sb, tb) = out[False], out[True]
+    same_rows = sum(a.tokens == b.tokens for a, b in zip(ra, rc))
+    _record("beam5 row-set decode (20 groups) large-v3 variable-length 60 windows",
+            dict(same_tokens=same_rows, stats=st_rows, all_rows_row_steps=ta["row_steps"]))
+    assert same_rows == W, same_rows
+    assert st_rows["refills"] == W - 20, st_rows
+    for a, b in zip(ra, rc):
+        assert abs(a.score - b.score) <= 1e-3 * max(1.0, abs(a.score))
+        assert abs(a.no_speech_prob - b.no_speech_prob) < 1e-4
     same = sum(a.tokens == b.tokens for a, b in zip(ra, rb))
     lens = [len(r.tokens) for r in ra]
     lens0 = [len(r.tokens) for r in ra]

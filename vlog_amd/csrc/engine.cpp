@@ -923,6 +923,7 @@ struct StepGraph {
 };
 
 void generate_rows(wm_engine* e, const wm_generate_args* a, hipStream_t st);
+void generate_rows_beam(wm_engine* e, const wm_generate_args* a, hipStream_t st);
 
 void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   check_weights(e);
@@ -946,7 +947,12 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     generate_rows(e, a, st);
     return;
   }
-  if (a->max_rows > 0 && a->max_rows < W) throw std::runtime_error("generate: max_rows needs greedy or num_hypotheses 1");
+  if (beam && a->max_rows > 0 && a->max_rows < NH) {
+    if (a->max_rows < per) throw std::runtime_error("generate: max_rows must hold one window's beam");
+    generate_rows_beam(e, a, st);
+    return;
+  }
+  if (a->max_rows > 0 && a->max_rows < W) throw std::runtime_error("generate: max_rows needs greedy, beam search or num_hypotheses 1");
   reserve(e, e->n_slots, NH);
   const bool rec = a->h_token_logprobs != nullptr;
   const int max_cand = beam ? std::max(1, (int)std::lround(a->beam_size * a->patience)) : 0;
@@ -1606,6 +1612,306 @@ void dtw_run(wm_engine* e, const float* d_x, int N, int M, int* h_i, int* h_j, i
   *h_len = n;
 }
 
+// Beam row-set decode: beam search over W windows with at most G = max_rows / K windows (groups of K hypothesis
+// slots) in flight.  A group decodes one window; when beam_select ends it (max_cand finished, max_length, or no live
+// beam), the host check reads the group's finished list and beams, finalises the window (openai's ranking, as
+// generate()) and starts the next window in the group: the event pass prefills the new window's prompt into the
+// group's first slot (P rows) beside the other groups' decode rows, and beam_start_kernel resets the group's state.
+// The K rows of a group stay together (its window's cross panels are read once for them), the row set keeps its
+// groups in place while windows wait (the step graph stays valid), and once nothing waits the finished groups'
+// rows are dropped at 7/8 (beam passes are GEMM-row-bound).  No per-step records in this form.
+void generate_rows_beam(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
+  const auto& m = e->dm;
+  const int C = m.n_text_ctx, V = m.n_vocab;
+  const int W = a->n_windows, P = a->prompt_len, K = a->beam_size;
+  const int G = std::max(1, std::min(a->max_rows / K, W));
+  const int NH = G * K;
+  const int ML = a->max_length;
+  const int max_cand = std::max(1, (int)std::lround(a->beam_size * a->patience));
+  if (max_cand > 16) throw std::runtime_error("generate: beam_size * patience must be <= 16");
+  if (a->h_token_logprobs) throw std::runtime_error("generate: per-step records need max_rows 0 with beam search");
+  reserve(e, e->n_slots, NH);
+  e->d_win_prompt.ensure((size_t)W * P * 4);
+  e->d_win_slot.ensure((size_t)W * 4);
+  e->d_res_ns.ensure((size_t)W * 4);
+  HIP_OK(hipMemcpyAsync(e->d_win_prompt.p, a->h_prompts, (size_t)W * P * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(e->d_win_slot.p, a->h_slots, (size_t)W * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemsetAsync(e->d_res_ns.p, 0, (size_t)W * 4, st));
+  HIP_OK(hipMemsetAsync(e->d_n_active.p, 0, 4 * 4, st));
+  {
+    std::vector<int> ones(NH, 1);              // every group starts ended (no window)
+    HIP_OK(hipMemcpyAsync(e->d_done.p, ones.data(), (size_t)NH * 4, hipMemcpyHostToDevice, st));
+    upload_suppress(e, a, st);                 // (synchronises: `ones` goes out of scope)
+  }
+  // pass rows: every hypothesis row + P prompt rows per starting group; logits rows: one per hypothesis row + one
+  // sot row per start
+  ensure_step(e, NH + G * std::max(P, K), NH + G);
+  float* logits = e->s_logits.as<float>();
+  int* counters = e->d_n_active.as<int>();
+  int* err = counters + 1;
+  SearchParams sp = search_params(e, a, logits, P);
+  sp.mode = 1; sp.topk = K + 1;
+  sp.row_hyp = e->d_row_hyp.as<int>();
+  BeamParams bp;
+  std::memset(&bp, 0, sizeof(bp));
+  bp.beam = K; bp.max_cand = max_cand; bp.n_ctx = C; bp.sample_begin = P; bp.max_length = ML;
+  bp.eot = m.eot; bp.cand_tok = sp.cand_tok; bp.cand_lp = sp.cand_lp; bp.tokens = sp.tokens; bp.lin = e->d_lin.as<int>();
+  bp.seq_len = sp.seq_len; bp.cum = sp.cum; bp.done = sp.done; bp.row_tok = sp.row_tok; bp.row_pos = sp.row_pos;
+  bp.fin_tok = e->d_fin_tok.as<int>(); bp.fin_len = e->d_fin_len.as<int>(); bp.fin_cum = e->d_fin_cum.as<float>();
+  bp.n_fin = e->d_n_fin.as<int>(); bp.n_active = sp.n_active;
+
+  // host view: the row set is a list of groups (K rows each, in order); group g decodes window gwin[g] while glive[g]
+  std::vector<int> set(G), gwin(G, -1);
+  std::vector<char> glive(G, 0), wdone(W, 0);
+  for (int g = 0; g < G; ++g) set[g] = g;
+  int next = 0, nfinal = 0;
+  long long passes = 0, row_steps = 0, refills = 0;
+  int captures = 0;
+  const float lp = a->length_penalty;
+  auto norm = [&](float c, int n) { return c / std::pow((float)std::max(n, 1), lp); };
+  // the finished groups' lists and beams -> their windows' results (openai finalize, as generate())
+  std::vector<int> f_tok, f_len, f_n, o_tok, o_len;
+  std::vector<float> f_cum, o_cum;
+  auto finalize = [&](const std::vector<int>& gs, hipStream_t s) {
+    if (gs.empty()) return;
+    f_tok.resize((size_t)G * max_cand * C); f_len.resize((size_t)G * max_cand); f_cum.resize((size_t)G * max_cand);
+    f_n.resize(G); o_tok.resize((size_t)NH * C); o_len.resize(NH); o_cum.resize(NH);
+    HIP_OK(hipMemcpyAsync(f_tok.data(), e->d_fin_tok.p, f_tok.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(f_len.data(), e->d_fin_len.p, f_len.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(f_cum.data(), e->d_fin_cum.p, f_cum.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(f_n.data(), e->d_n_fin.p, (size_t)G * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(o_tok.data(), e->d_tokens.p, o_tok.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(o_len.data(), e->d_seq_len.p, (size_t)NH * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(o_cum.data(), e->d_cum.p, (size_t)NH * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    for (int g : gs) {
+      const int w = gwin[g];
+      struct C2 { const int* t; int n; float c; };
+      std::vector<C2> cands;
+      for (int i = 0; i < std::min(f_n[g], max_cand); ++i) {
+        const size_t f = (size_t)g * max_cand + i;
+        cands.push_back({&f_tok[f * C], f_len[f], f_cum[f]});
+      }
+      if ((int)cands.size() < K) {
+        std::vector<int> order;
+        for (int b = 0; b < K; ++b)
+          if (o_cum[g * K + b] > -INFINITY) order.push_back(b);
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return o_cum[g * K + x] > o_cum[g * K + y]; });
+        for (int b : order) {
+          if ((int)cands.size() >= K) break;
+          const int h = g * K + b;
+          cands.push_back({&o_tok[(size_t)h * C + P], o_len[h] - P, o_cum[h]});
+        }
+      }
+      int best_len = 0;
+      float best_cum = 0.f, best_score = -INFINITY;
+      const int* best_ptr = nullptr;
+      for (const auto& c : cands) {
+        const float sc = norm(c.c, c.n);
+        if (sc > best_score) { best_score = sc; best_len = c.n; best_cum = c.c; best_ptr = c.t; }
+      }
+      if (best_len < 0 || best_len > ML) throw std::runtime_error("generate: window " + std::to_string(w) + " has no result");
+      for (int i = 0; i < best_len; ++i) a->h_tokens[(size_t)w * ML + i] = best_ptr[i];
+      a->h_lengths[w] = best_len;
+      a->h_scores[w] = best_score;
+      if (a->h_cum_logprob) a->h_cum_logprob[w] = best_cum;
+      wdone[w] = 1;
+      ++nfinal;
+      glive[g] = 0;
+      gwin[g] = -1;
+    }
+  };
+
+  // One event pass: `starts` (group, window) begin in place; `nset` is the new row set (compaction drops groups).
+  std::vector<int> nset;
+  std::vector<std::pair<int, int>> starts;
+  int nrows = NH;
+  // A starting group's P prompt rows are padded to K with copies of its last prompt row (same hypothesis, position
+  // and token: identical self-KV writes), so every group of the pass holds K rows of one window and the
+  // cross-attention keeps its per-window grouping (prompts longer than K rows: ungrouped rows).
+  const int PR = std::max(P, K);
+  const int ev_group = P <= K ? K : 1;
+  auto event = [&](hipStream_t s) {
+    const int ng = (int)nset.size(), nr = ng * K, nst = (int)starts.size();
+    const int nsot = a->sot_index >= 0 ? nst : 0;
+    std::vector<int> start_of(G, -1);
+    for (int k = 0; k < nst; ++k) start_of[starts[k].first] = k;
+    int np = 0, n_live = 0;
+    for (int g : nset) {
+      np += start_of[g] >= 0 ? (ev_group > 1 ? PR : P) : K;
+      n_live += (start_of[g] >= 0 || glive[g]) ? K : 0;
+    }
+    std::vector<int>& u = e->h_ev;
+    u.assign((size_t)4 * np + 2 * nr + nsot + 2 * nst + 1, 0);
+    int* ptok = u.data(); int* ppos = ptok + np; int* phyp = ppos + np; int* psrc = phyp + np;
+    int* rh = psrc + np; int* lr = rh + nr; int* gsd = lr + nr + nsot; int* wsd = gsd + nst;
+    wsd[nst] = n_live;
+    int i = 0, r = 0;
+    for (int g : nset) {
+      const int h0 = g * K, k = start_of[g];
+      if (k >= 0) {
+        const int w = starts[k].second;
+        int last = 0;
+        for (int p = 0; p < P; ++p, ++i) {
+          ptok[i] = a->h_prompts[(size_t)w * P + p]; ppos[i] = p; phyp[i] = h0; psrc[i] = -1;
+          if (p == a->sot_index) lr[nr + k] = i;
+          last = i;
+        }
+        for (int p = P; ev_group > 1 && p < PR; ++p, ++i) {
+          ptok[i] = a->h_prompts[(size_t)w * P + P - 1]; ppos[i] = P - 1; phyp[i] = h0; psrc[i] = -1;
+        }
+        for (int b = 0; b < K; ++b, ++r) { rh[r] = h0 + b; lr[r] = last; }
+        gsd[k] = g; wsd[k] = w;
+      } else {
+        for (int b = 0; b < K; ++b, ++i, ++r) {
+          phyp[i] = h0 + b; psrc[i] = h0 + b;
+          rh[r] = h0 + b; lr[r] = i;
+        }
+      }
+    }
+    e->d_ev.ensure(u.size() * 4);
+    int* du = e->d_ev.as<int>();
+    HIP_OK(hipMemcpyAsync(du, u.data(), u.size() * 4, hipMemcpyHostToDevice, s));
+    int* dptok = du; int* dppos = du + np; int* dphyp = du + 2 * np; int* dpsrc = du + 3 * np;
+    int* drh = du + 4 * np; int* dlr = drh + nr; int* dgs = dlr + nr + nsot; int* dws = dgs + nst;
+    // carried rows: token / position of their hypothesis from the last beam selection (hypothesis-indexed)
+    launch_rows_fill(np, dpsrc, dptok, dppos, e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), s);
+    launch_beam_start(nst, dgs, dws, K, e->d_win_prompt.as<int>(), P, e->d_win_slot.as<int>(), C, e->d_tokens.as<int>(),
+                      e->d_lin.as<int>(), e->d_seq_len.as<int>(), e->d_done.as<int>(), e->d_cum.as<float>(),
+                      e->d_hyp_slot.as<int>(), e->d_n_fin.as<int>(), s);
+    HIP_OK(hipMemcpyAsync(e->d_row_hyp.p, drh, (size_t)nr * 4, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipMemcpyAsync(counters, dws + nst, 4, hipMemcpyDeviceToDevice, s));
+    decoder_pass(e, np, dptok, dppos, dphyp, e->d_done.as<int>(), e->d_lin.as<int>(), dlr, nr + nsot, logits, nullptr, 0,
+                 nullptr, ev_group, s, err);
+    if (nsot) launch_no_speech(logits + (size_t)nr * V, V, V, nsot, m.no_speech, e->d_res_ns.as<float>(), s, dws);
+    debug_nan(e, logits, nr, s);
+    {
+      ProfScope ps(e, P_SELECT, s);
+      launch_logits_select(sp, nr, s);
+      launch_beam_select(bp, G, s);
+    }
+    for (const auto& gw : starts) { gwin[gw.first] = gw.second; glive[gw.first] = 1; }
+    set = nset;
+    nrows = nr;
+    ++passes;
+    row_steps += nr;
+  };
+
+  const bool use_graph = e->dec_graph && !e->prof_on && !e->dec_split;
+  hipStream_t ds = st;
+  if (use_graph) {
+    if (!e->gst) {
+      HIP_OK(hipStreamCreateWithFlags(&e->gst, hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_g0, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&e->ev_g1, hipEventDisableTiming));
+    }
+    HIP_OK(hipEventRecord(e->ev_g0, st));
+    HIP_OK(hipStreamWaitEvent(e->gst, e->ev_g0, 0));
+    ds = e->gst;
+  }
+  auto step_eager = [&](hipStream_t s) {
+    launch_rows_fill(nrows, e->d_row_hyp.as<int>(), e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(),
+                     e->d_row_tok.as<int>(), e->d_row_pos.as<int>(), s);
+    decoder_pass(e, nrows, e->d_prow_tok.as<int>(), e->d_prow_pos.as<int>(), e->d_row_hyp.as<int>(), e->d_done.as<int>(),
+                 e->d_lin.as<int>(), nullptr, nrows, logits, nullptr, 0, nullptr, K, s, err);
+    debug_nan(e, logits, nrows, s);
+    ProfScope ps(e, P_SELECT, s);
+    launch_logits_select(sp, nrows, s);
+    launch_beam_select(bp, G, s);
+  };
+
+  StepGraph graph;
+  bool graph_rows_changed = true;
+  const int check = std::max(1, a->check_every);
+  const int refill_min = std::max(1, G / 16);
+  std::vector<int> h_done(NH);
+  int h_cnt[4] = {0, 0, 0, 0};
+  const long long pass_limit = (long long)(W / G + 2) * (ML - P + check + 2) + 16;
+  try {
+    nset = set;
+    starts.clear();
+    for (int g = 0; g < G; ++g) starts.push_back({g, next++});
+    event(ds);
+    int k = 1;
+    for (;;) {
+      if (k >= check) {
+        k = 0;
+        HIP_OK(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, ds));
+        HIP_OK(hipMemcpyAsync(h_done.data(), e->d_done.p, (size_t)NH * 4, hipMemcpyDeviceToHost, ds));
+        HIP_OK(hipStreamSynchronize(ds));
+        check_decode_error(h_cnt + 1);
+        std::vector<int> ended;
+        for (int g = 0; g < G; ++g)
+          if (glive[g] && h_done[g * K]) ended.push_back(g);
+        finalize(ended, ds);
+        int n_live = 0, n_free = 0;
+        for (int g : set) { n_live += glive[g]; n_free += !glive[g]; }
+        if (n_live == 0 && next >= W) break;
+        const bool refill = next < W && (n_free >= refill_min || n_live == 0);
+        const bool compact = next >= W && n_live * 8 <= (int)set.size() * 7;
+        if (refill || compact) {
+          nset.clear(); starts.clear();
+          for (int g : set) {
+            if (glive[g]) nset.push_back(g);
+            else if (refill && next < W) { nset.push_back(g); starts.push_back({g, next++}); ++refills; }
+            else if (refill) nset.push_back(g);       // idle until compaction (rows stay in place)
+          }
+          const int before = nrows;
+          event(ds);
+          if (nrows != before) {
+            graph.drop();
+            graph_rows_changed = true;
+          }
+          k = 1;
+          continue;
+        }
+      }
+      if (!graph.valid()) {
+        graph.drop();
+        graph_rows_changed = true;
+      }
+      if (!use_graph || graph_rows_changed) {
+        step_eager(ds);
+        graph_rows_changed = false;
+      } else {
+        if (!graph.exec) ++captures;
+        graph.run(ds, [&] { step_eager(ds); });
+      }
+      ++passes;
+      row_steps += nrows;
+      ++k;
+      if (passes > pass_limit) throw std::runtime_error("generate: decode did not terminate");
+    }
+  } catch (...) {
+    graph.abort(ds);
+    throw;
+  }
+  if (use_graph) {
+    HIP_OK(hipEventRecord(e->ev_g1, ds));
+    HIP_OK(hipStreamWaitEvent(st, e->ev_g1, 0));
+  }
+  if (graph.exec) {
+    HIP_OK(hipStreamSynchronize(ds));
+    graph.drop();
+  }
+  std::vector<float> res_ns(W);
+  HIP_OK(hipMemcpyAsync(res_ns.data(), e->d_res_ns.p, (size_t)W * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  check_decode_error(h_cnt + 1);
+  if (nfinal != W) throw std::runtime_error("generate: beam row-set finished " + std::to_string(nfinal) + " of " +
+                                            std::to_string(W) + " windows");
+  for (int w = 0; w < W; ++w)
+    if (a->h_no_speech) a->h_no_speech[w] = res_ns[w];
+  if (a->h_steps) a->h_steps[0] = (int)passes;
+  if (a->h_stats) {
+    a->h_stats[0] = passes;
+    a->h_stats[1] = row_steps;
+    a->h_stats[2] = refills;
+    a->h_stats[3] = captures;
+  }
+}
+
 void align(wm_engine* e, int slot, int sot_len, const int* h_sot, int n_text, const int* h_text, int num_frames,
            const int* h_heads, int n_heads, int medw, float* h_probs, int* h_ti, int* h_tj, int* h_len, hipStream_t st) {
   const auto& m = e->dm;
@@ -1667,6 +1973,11 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
   HIP_OK(hipMemGetInfo(&free_b, &total_b));
   const double reusable = (double)e->a_attn.bytes + (double)e->a_logits.bytes;
   const double budget = std::max(1.5e9, std::min(48e9, 0.5 * (double)free_b + reusable));
+  static const bool align_log = [] {
+    const char* v = std::getenv("VLOG_AMD_ALIGN_LOG");
+    return v && v[0] == '1';
+  }();
+  if (align_log) std::fprintf(stderr, "[align_batch] %d items, free %.1f GB, budget %.1f GB\n", n, free_b / 1e9, budget / 1e9);
   // Items longest-first, chunked so padding (every sequence of a chunk padded to its longest) stays under a
   // quarter of the chunk's rows: with transcripts of 5 to 220 tokens one padded pass would run ~2x the rows.
   std::vector<int> ord(n);

@@ -70,6 +70,9 @@ void launch_hyp_start(int n, const int* hs, const int* ws, const int* win_prompt
                       int* tokens, int* seq_len, int* done, float* cum, int* hyp_slot, int* hyp_out, hipStream_t st);
 // Pass rows whose token / position live on the device: row i with src[i] >= 0 takes (row_tok, row_pos)[src[i]].
 void launch_rows_fill(int n, const int* src, int* tok, int* pos, const int* row_tok, const int* row_pos, hipStream_t st);
+void launch_beam_start(int n, const int* gs, const int* ws, int K, const int* win_prompt, int P, const int* win_slot,
+                       int n_ctx, int* tokens, int* lin, int* seq_len, int* done, float* cum, int* hyp_slot, int* n_fin,
+                       hipStream_t st);
 
 // one block per row (n_rows = hypotheses, or the compacted row set's rows with p.row_hyp)
 void launch_logits_select(const SearchParams& p, int n_rows, hipStream_t st);

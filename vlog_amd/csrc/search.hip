@@ -494,6 +494,40 @@ void launch_hyp_start(int n, const int* hs, const int* ws, const int* win_prompt
   WM_LAUNCH_CHECK("hyp_start_kernel");
 }
 
+// Beam row-set decode: group gs[i] of K hypothesis slots starts window ws[i]: every hypothesis gets the window's
+// prompt, its lineage points the prompt positions at the group's first slot (whose self-KV the pass prefills), the
+// first slot carries the score (the others start dead, as the one-pass beam prefill), and the group's finished list
+// is emptied.
+__global__ __launch_bounds__(256) void beam_start_kernel(const int* __restrict__ gs, const int* __restrict__ ws, int K,
+                                                         const int* __restrict__ win_prompt, int P,
+                                                         const int* __restrict__ win_slot, int n_ctx, int* tokens,
+                                                         int* lin, int* seq_len, int* done, float* cum, int* hyp_slot,
+                                                         int* n_fin) {
+  const int g = gs[blockIdx.x], w = ws[blockIdx.x], h0 = g * K;
+  for (int i = threadIdx.x; i < K * P; i += blockDim.x) {
+    const int b = i / P, p = i - b * P;
+    tokens[(long long)(h0 + b) * n_ctx + p] = win_prompt[(long long)w * P + p];
+    lin[(long long)(h0 + b) * n_ctx + p] = h0;
+  }
+  if (threadIdx.x < K) {
+    const int h = h0 + threadIdx.x;
+    seq_len[h] = P;
+    done[h] = 0;
+    cum[h] = threadIdx.x == 0 ? 0.f : -INFINITY;
+    hyp_slot[h] = win_slot[w];
+  }
+  if (threadIdx.x == 0) n_fin[g] = 0;
+}
+
+void launch_beam_start(int n, const int* gs, const int* ws, int K, const int* win_prompt, int P, const int* win_slot,
+                       int n_ctx, int* tokens, int* lin, int* seq_len, int* done, float* cum, int* hyp_slot, int* n_fin,
+                       hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(beam_start_kernel, dim3(n), dim3(256), 0, st, gs, ws, K, win_prompt, P, win_slot, n_ctx, tokens,
+                     lin, seq_len, done, cum, hyp_slot, n_fin);
+  WM_LAUNCH_CHECK("beam_start_kernel");
+}
+
 __global__ __launch_bounds__(256) void rows_fill_kernel(int n, const int* __restrict__ src, int* __restrict__ tok,
                                                         int* __restrict__ pos, const int* __restrict__ row_tok,
                                                         const int* __restrict__ row_pos) {
