@@ -600,8 +600,9 @@ def main():
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
                    "token_length_min_p50_max": [int(np.min(toks)), int(np.median(toks)), int(np.max(toks))],
-                   "decode": (f"continuous row-set over the {args.steps} batches ({W} rows, longest-expected first, "
-                              f"refill across batches + compaction)" if args.stream else
+                   "decode": (f"continuous row-set over the {args.steps} batches "
+                              f"({W} windows in flight{' x %d beam rows' % args.beam if args.beam > 1 else ''}, "
+                              f"longest-expected first, refill across batches + compaction)" if args.stream else
                               "all-rows batch" if args.max_rows < 0 else
                               f"row-set (max_rows {args.max_rows or W}, longest-expected first, refill + compaction)"),
                    "decoder_row_steps": pipe.last["gen_stats"].get("row_steps"),
