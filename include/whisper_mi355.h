@@ -148,8 +148,10 @@ typedef struct wm_generate_args {
    * window is waiting, finished rows are dropped from the passes when the live rows fall to 5/8 of the pass (the
    * step graph is re-captured for the new row count).  Each window's result is the same computation either way;
    * the GEMM / attention routes follow the pass's row count, so results agree to f32 rounding, not bit for bit.
-   * Beam search: compact = 1 drops the hypotheses of finished windows from the passes the same way (when the live
-   * hypotheses fall to 7/8 of the pass); max_rows must stay 0. */
+   * Beam search: max_rows (a multiple of beam_size is used: max_rows / beam_size windows in flight) refills a
+   * finished window's group of beam_size rows with the next window (no per-step records in this form); compact = 1
+   * drops the hypotheses of finished windows from the passes once nothing waits (when the live hypotheses fall to
+   * 7/8 of the pass). */
   int32_t max_rows;
   int32_t compact;
   /* Optional per-step records, [n_windows][max_length] (NULL: off): the log-prob (after the logit rules) of the
