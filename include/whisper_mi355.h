@@ -274,6 +274,8 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "cross_mfma" (default 1): projected form, decode passes whose windows have 2..32 rows (beam hypotheses, prompt
  *   prefill) run the cross-attention on the same matrix-core kernel, the keys split over blocks to fill the chip and
  *   merged by the split-combine kernel; 0 = the f32 VALU group kernel.  Changes numerics at bf16-rounding level.
+ *   "cross_mfma_fuse" (default 0): 1 = that merge done inside the kernel by the last-arriving key split (same
+ *   arithmetic and order, bit-identical output; measured ~6 % slower per cross-attention than the separate kernel).
  *   "debug_nan_row" (default -1, TEST ONLY): >= 0 overwrites logits row r of every decode pass of wm_generate with
  *   NaN before token selection (exercises the failure contract of wm_generate). */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);

@@ -14,6 +14,7 @@ from vlog_amd.weights import synthetic_state_dict
 pytestmark = pytest.mark.gpu
 
 W = 40
+_ENC = []      # the fixture's encoder output (tests that switch the cross form re-fill the slots from it)
 
 
 @pytest.fixture(scope="module")
@@ -27,23 +28,25 @@ def batch():
     enc = eng.encode(torch.from_numpy(feats).cuda(), [3000 * i for i in range(W)], [3000] * W)
     eng.reserve(W, 5 * W)
     eng.cross_kv(enc, 0)
+    _ENC.append(enc)
     return dims, eng
 
 
-def _run(eng, dims, split, opts=(), **kw):
+def _run(eng, dims, split, opts=(), windows=W, **kw):
     st = dims.specials
     eng.set_option("decode_split", split)
     for k, v in opts:
         eng.set_option(k, v)
     prompt = [st.sot, st.lang_token("en"), st.transcribe]
     sup = [st.transcribe, st.translate, st.sot, st.sot_prev, st.sot_lm]
-    res, steps = eng.generate(list(range(W)), [prompt] * W, suppress_tokens=sup, max_length=120, **kw)
+    res, steps = eng.generate(list(range(windows)), [prompt] * windows, suppress_tokens=sup, max_length=120, **kw)
     eng.set_option("decode_split", 0)                 # back to the defaults
     eng.set_option("cross_attn_fuse", 1)
     eng.set_option("cross_attn_blocks", 0)
     eng.set_option("cross_attn_snake", 0)
     eng.set_option("cross_attn_keep", 0)
     eng.set_option("decode_gemm_plan", 1)          # also restores the preset's column widths
+    eng.set_option("cross_mfma_fuse", 0)
     return res, steps
 
 
@@ -64,6 +67,25 @@ def test_cross_attention_forms_bit_identical(batch, kw, opts):
     a, sa = _run(eng, dims, 0, **kw)
     b, sb = _run(eng, dims, 0, opts=opts, **kw)
     _same(a, sa, b, sb)
+
+
+@pytest.mark.parametrize("windows", [2, W])
+def test_mfma_beam_combine_fused_bit_identical(batch, windows):
+    """Projected form, beam groups on the matrix-core cross-attention: the key-split merge done by the last-arriving
+    split inside the kernel (cross_mfma_fuse=1) vs the separate combine kernel: same arithmetic and order, so the
+    same tokens, scores and no-speech probabilities (2 windows: 16 key splits; 40 windows: 3)."""
+    dims, eng = batch
+    kw = dict(beam_size=5, patience=1.0)
+    eng.set_option("cross_mode", 0)             # the product's form for beam groups (transcribe.py)
+    try:
+        eng.cross_kv(_ENC[0], 0)
+        a, sa = _run(eng, dims, 0, windows=windows, **kw)
+        b, sb = _run(eng, dims, 0, opts=(("cross_mfma_fuse", 1),), windows=windows, **kw)
+    finally:
+        eng.set_option("cross_mode", 1)
+        eng.cross_kv(_ENC[0], 0)
+    _same(a, sa, b, sb)
+    assert sum(len(r.tokens) for r in a) > windows * 5
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(beam_size=5, patience=1.0)], ids=["greedy", "beam5"])

@@ -222,6 +222,35 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
   out[(long long)row * ldo + h * HD + e] = f2bf(o / L);
 }
 
+// The key-split merge of one (row, head, element) from partials another block wrote through to L2 (agent-scope
+// loads): cross_combine_kernel's arithmetic and order, every load requested before any is used (clamped indices,
+// no per-split branch: a branch per split made each load wait for the previous one, ~16 round trips at 16 splits)
+__device__ __forceinline__ float combine_l2(const float* part_m, const float* part_l, const float* part_o,
+                                            long long pb, int splits, int e) {
+  constexpr int SMAX = 16;
+  float pm[SMAX], pl[SMAX], po[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) {
+    const long long q = pb + (s < splits ? s : 0);
+    pm[s] = __hip_atomic_load(part_m + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pl[s] = __hip_atomic_load(part_l + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    po[s] = __hip_atomic_load(part_o + q * HD + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s)
+    if (s < splits) M = fmaxf(M, pm[s]);
+  float L = 0.f, o = 0.f;
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s)
+    if (s < splits) {
+      const float w = exp2f(pm[s] - M);
+      L += pl[s] * w;
+      o += po[s] * w;
+    }
+  return o / L;
+}
+
 // ------------------------------------------------------------------------------------------------------
 // Cross-attention, single pass (flash decoding) over RG query rows that share one window slot — the
 // beam hypotheses of a window, or the prompt positions of a prefill — so each (slot, head) K/V panel is
@@ -426,22 +455,13 @@ __device__ __forceinline__ void cross_item(const DecAttnArgs& a, int bx, int spl
     }
     __syncthreads();
     if (s_last) {
-      // same arithmetic and order as cross_combine_kernel; every load of the partials is an sc1 load
+      // same arithmetic and order as cross_combine_kernel (combine_l2)
       for (int idx = tid; idx < RG * HD; idx += 256) {
         const int r = idx / HD, e = idx - r * HD;
         const int row = row0 + r;
         if (a.done && a.done[a.row_hyp[row]]) continue;
         const long long pb = ((long long)row * H + h) * a.splits;
-        float M = -INFINITY;
-        for (int sp = 0; sp < a.splits; ++sp)
-          M = fmaxf(M, __hip_atomic_load(a.part_m + pb + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        float L = 0.f, O = 0.f;
-        for (int sp = 0; sp < a.splits; ++sp) {
-          const float w = exp2f(__hip_atomic_load(a.part_m + pb + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - M);
-          L += __hip_atomic_load(a.part_l + pb + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * w;
-          O += __hip_atomic_load(a.part_o + (pb + sp) * HD + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * w;
-        }
-        a.out[(long long)row * a.ldo + h * HD + e] = f2bf(O / L);
+        a.out[(long long)row * a.ldo + h * HD + e] = f2bf(combine_l2(a.part_m, a.part_l, a.part_o, pb, a.splits, e));
       }
     }
   }
@@ -971,6 +991,47 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
     __syncthreads();
   }
   if (!cap) l_run += __shfl_xor(l_run, 32, 64);
+  if (a.splits > 1 && a.cnt) {
+    // the combine folded in: every split writes its partial through to L2 (agent-scope stores), drains, and takes
+    // one ticket per (group, head, row tile); the last arriver combines with cross_combine_kernel's arithmetic and
+    // order (bit-identical to the separate kernel) and re-arms the counter (cdna_hip_programming.md §6 Guideline 16)
+    if (valid) {
+      const long long pi = ((long long)(row0 + r) * H + h) * a.splits + sp;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            __hip_atomic_store(a.part_o + pi * HD + 32 * hb + 8 * gg + 4 * hh + j, o[hb][4 * gg + j],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (hh == 0) {
+        __hip_atomic_store(a.part_m + pi, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.part_l + pi, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      int* c = a.cnt + (g * H + h) * nqt + qt;
+      const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == a.splits - 1;
+      if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const int nr = min(128, group - qt * 128);
+    for (int idx = tid; idx < nr * HD; idx += 256) {
+      const int rr = idx / HD, e = idx - rr * HD;
+      const int row = row0 + qt * 128 + rr;
+      if (a.done && a.done[a.row_hyp[row]]) continue;
+      const long long pb = ((long long)row * H + h) * a.splits;
+      a.out[(long long)row * a.ldo + h * HD + e] = f2bf(combine_l2(a.part_m, a.part_l, a.part_o, pb, a.splits, e));
+    }
+    return;
+  }
   if (valid && a.splits > 1) {
     // partial of this key split (unnormalised o, its max and sum in log2 units) for cross_combine_kernel
     const long long pi = ((long long)(row0 + r) * H + h) * a.splits + sp;
@@ -1066,14 +1127,16 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
       splits = std::max(1, std::min(std::min(16, ntt), (512 + plan_blocks - 1) / plan_blocks));
     }
     a.splits = splits;
+    // in-kernel combine only for decode key splits (one row tile per group: the counters are rows/group x H)
+    a.cnt = mf_dec && nqt == 1 ? fz.tf_cnt : nullptr;
     const long long nblk = (long long)(rows / group) * H * nqt * splits;
     if (nblk > (1LL << 31) - 1) throw std::runtime_error("cross_attn: grid too large");
     if (splits > 1 && (!part_m || !part_l || !part_o)) throw std::runtime_error("cross_attn: no split scratch");
-    hipEvent_t e1 = splits == 1 ? ev1 : nullptr;
+    hipEvent_t e1 = (splits == 1 || a.cnt) ? ev1 : nullptr;
     if (ev0) hipExtLaunchKernelGGL(cross_tf_kernel, dim3((unsigned)nblk), dim3(256), 0, st, ev0, e1, 0, a, group, nqt);
     else hipLaunchKernelGGL(cross_tf_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a, group, nqt);
     WM_LAUNCH_CHECK("cross_tf_kernel");
-    if (splits > 1) {
+    if (splits > 1 && !a.cnt) {
       if (ev1)
         hipExtLaunchKernelGGL(cross_combine_kernel, dim3(rows * H), dim3(HD), 0, st, nullptr, ev1, 0, part_m, part_l,
                               part_o, row_hyp, done, out, ldo, H, splits);

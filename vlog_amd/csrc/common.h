@@ -62,6 +62,8 @@ struct CrossFuse {
   int* cnt = nullptr;              // >= rows*H zeroed ints (nullptr: separate combine kernel)
   int tf = 0;                      // teacher-forced pass (`group` contiguous rows per window): matrix-core kernel
   int mfma = 0;                    // decode pass: row groups of 2..32 rows per window on the matrix-core kernel
+  int* tf_cnt = nullptr;           // matrix-core decode pass: >= rows*H zeroed ints, the key-split combine done by
+                                   // the last-arriving split in-kernel (nullptr: separate combine kernel)
 };
 
 // Launch check used by every host-side launcher: converts an asynchronous launch failure into an

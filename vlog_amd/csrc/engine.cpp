@@ -195,6 +195,9 @@ struct wm_engine {
   int cross_mode = 1;
   int cross_tf = 1;          // teacher-forced passes (alignment) run the projected form's cross-attention on MFMA
   int cross_mfma = 1;        // projected form, decode passes with 2..32 rows per window (beam groups): MFMA kernel
+  int cross_mfma_fuse = 0;   // ... its key-split combine done by the last-arriving split (d_cross_cnt), not a kernel:
+                             // measured slower (16.3 vs 15.3 us per layer at 1 window, beam 5: the L2 hand-off
+                             // costs ~3 round trips, more than the combine kernel behind it in the stream)
   int dec_big_rows = 320;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
                              // whole K per block (decoder_layer)
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
@@ -614,6 +617,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   if ((e->cross_fuse & 2) && e->cross_mode == 0) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   fz.tf = (attn && align_map && e->cross_tf) ? 1 : 0;
   fz.mfma = e->cross_mfma;
+  if (e->cross_mfma_fuse && e->cross_mode == 0) fz.tf_cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   float* probs = nullptr;
   const int* hmap = nullptr;
   if (attn && align_map) {
@@ -2472,6 +2476,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "debug_nan_row") e->dbg_nan_row = (int)std::max<int64_t>(-1, std::min<int64_t>(value, 1 << 30));
     else if (k == "cross_tf") e->cross_tf = value ? 1 : 0;
     else if (k == "cross_mfma") e->cross_mfma = value ? 1 : 0;
+    else if (k == "cross_mfma_fuse") e->cross_mfma_fuse = value ? 1 : 0;
     else if (k == "decode_gemm_big_rows") e->dec_big_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
@@ -2513,6 +2518,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "debug_nan_row") *value = e->dbg_nan_row;
     else if (k == "cross_tf") *value = e->cross_tf;
     else if (k == "cross_mfma") *value = e->cross_mfma;
+    else if (k == "cross_mfma_fuse") *value = e->cross_mfma_fuse;
     else if (k == "decode_gemm_big_rows") *value = e->dec_big_rows;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
   });
