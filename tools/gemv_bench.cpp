@@ -99,6 +99,46 @@ int main(int argc, char** argv) {
   };
   std::printf("empty kernel chain (320 x 256)       %7.2f us\n",
               timeit([&](int) { hipLaunchKernelGGL(empty_kernel, dim3(320), dim3(256), 0, st, 0); }));
+  if (std::getenv("GB_PRODUCT")) {
+    // the product's forms at M = 5 (engine decoder_layer with decode_gemv_ln): the residual producer with row
+    // statistics, and the LayerNorm-consuming cq (slabs left for the attention kernel) and fc1, each against the
+    // plain bf16-operand form of the same shape
+    const int M = 5;
+    gemv_set_target_blocks(256);
+    float* dStat;
+    CK(hipMalloc(&dStat, (size_t)128 * 32 * 2 * 4));
+    CK(hipMemset(dStat, 0, (size_t)128 * 32 * 2 * 4));
+    auto run = [&](const char* name, int N, int K, int kind, bool lna, bool stat, bool defer) {
+      GemmEpi ep;
+      std::memset(&ep, 0, sizeof(ep));
+      ep.kind = kind;
+      ep.out = kind == EPI_RESID_F32 ? (void*)dX : (void*)dC;
+      ep.ldc = kind == EPI_RESID_F32 ? 1280 : N;
+      if (stat) ep.stat_out = dStat;
+      ep.defer_combine = defer;
+      GemmA a{dA, (long long)K, 0, 0};
+      if (lna) { a.lnx = dX; a.ld = 1280; a.ln_g = dG; a.ln_b = dB; a.ln_stat = dStat; a.ln_tiles = 80; }
+      const double us = timeit([&](int r) {
+        if (!launch_dec_gemv(a, dW + maxW * (r % NCOPY), K, M, N, K, ep, ws, wsb, st)) std::exit(3);
+      });
+      std::printf("product M=%d %-28s N=%5d K=%5d  %6.2f us  %6.0f GB/s\n", M, name, N, K, us, 2.0 * N * K / us / 1e3);
+    };
+    run("out  resid+stat", 1280, 1280, EPI_RESID_F32, false, true, false);
+    run("cq   plain, slabs deferred", 1280, 1280, EPI_BF16, false, false, true);
+    run("fc1  plain", 5120, 1280, EPI_BF16, false, false, false);
+    run("qkv  plain (bf16 out)", 3840, 1280, EPI_BF16, false, false, false);
+    // LayerNorm-operand ablations (gemv_set_ablation): 1 no statistics loads, 2 activation loads of rows < M only,
+    // 4 no affine loads, 8 no statistics LDS rounds
+    for (int abl : {0, 1, 2, 4, 8, 15}) {
+      gemv_set_ablation(abl);
+      std::printf("ablation %2d\n", abl);
+      run("cq   LN operand, slabs deferred", 1280, 1280, EPI_BF16, true, false, true);
+      run("fc1  LN operand", 5120, 1280, EPI_BF16, true, false, false);
+      run("qkv  LN operand (bf16 out)", 3840, 1280, EPI_BF16, true, false, false);
+    }
+    gemv_set_ablation(0);
+    return 0;
+  }
   for (int M : {5, 16}) {
     for (int target : {64, 128, 256}) {
       gemv_set_target_blocks(target);

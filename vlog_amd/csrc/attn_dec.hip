@@ -810,31 +810,6 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
   const int r = qt * 128 + wv * 32 + ql;
   const bool valid = r < group;
   const bool wave_on = qt * 128 + wv * 32 < group;     // wave-uniform: a wave with no row only stages tiles
-  bf16x8 qf[4];
-  if (a.q_part) {
-    // q = bf16(sum of the cq split-K slabs in slab order + bias), as splitk_reduce_kernel forms it (bit-identical
-    // to the unfused bf16 q); every slab load of the lane is issued before the adds
-    const long long slab = (long long)a.q_rows * a.ldq;
-    const float* qp = a.q_part + (long long)(row0 + min(r, group - 1)) * a.ldq + h * HD + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
-      for (int k = 0; k < a.q_splits; ++k) {
-        v0 += *(const f32x4*)(qp + k * slab + 16 * s);
-        v1 += *(const f32x4*)(qp + k * slab + 16 * s + 4);
-      }
-      const float* bq = a.q_bias + h * HD + 8 * hh + 16 * s;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        qf[s][j] = f2bf(v0[j] + bq[j]);
-        qf[s][4 + j] = f2bf(v1[j] + bq[4 + j]);
-      }
-    }
-  } else {
-    const bf16* qp = a.q + (long long)(row0 + min(r, group - 1)) * a.ldq + h * HD + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-  }
   const float sl2 = a.scale_log2;
   const int ntt = (T + TF_KT - 1) / TF_KT;
   const int tb = sp * ntt / a.splits, te = (sp + 1) * ntt / a.splits;   // this split's key tiles
@@ -858,6 +833,54 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
       if (withv) *(i32x4*)(sV + tf_vslot(rr, ch)) = rv[i];
     }
   };
+  // (requesting the first tile's K and V before the q load, as cross_item does, measured 2 % slower here: 111.5 vs
+  // 109.5 ms of cross-attention per 60 s beam-5 call, alternating arms on one box)
+  bf16x8 qf[4];
+  if (a.q_part) {
+    // q = bf16(sum of the cq split-K slabs in slab order + bias), as splitk_reduce_kernel forms it (bit-identical
+    // to the unfused bf16 q).  Slabs in chunks of QC, every load of a chunk issued before its adds, indices clamped
+    // instead of branched (a runtime loop per slab waited one round trip per slab and 16-column group: 16 at 4 slabs)
+    const long long slab = (long long)a.q_rows * a.ldq;
+    const float* qp = a.q_part + (long long)(row0 + min(r, group - 1)) * a.ldq + h * HD + 8 * hh;
+    constexpr int QC = 4;
+    f32x4 v0[4], v1[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) v0[s] = v1[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < a.q_splits; k0 += QC) {
+      f32x4 t0[QC][4], t1[QC][4];
+#pragma unroll
+      for (int j = 0; j < QC; ++j) {
+        const float* pk = qp + (long long)min(k0 + j, a.q_splits - 1) * slab;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          t0[j][s] = *(const f32x4*)(pk + 16 * s);
+          t1[j][s] = *(const f32x4*)(pk + 16 * s + 4);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < QC; ++j) {
+        const bool use = k0 + j < a.q_splits;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          v0[s] = use ? v0[s] + t0[j][s] : v0[s];
+          v1[s] = use ? v1[s] + t1[j][s] : v1[s];
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float* bq = a.q_bias + h * HD + 8 * hh + 16 * s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        qf[s][j] = f2bf(v0[s][j] + bq[j]);
+        qf[s][4 + j] = f2bf(v1[s][j] + bq[4 + j]);
+      }
+    }
+  } else {
+    const bf16* qp = a.q + (long long)(row0 + min(r, group - 1)) * a.ldq + h * HD + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  }
   // S^T of the tile's two 32-key blocks, scaled to log2 units, keys past T masked
   auto scores = [&](const bf16* sK, int t, f32x16 (&sc)[2]) {
 #pragma unroll

@@ -90,6 +90,7 @@ bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int
 // gemv_splits: the split count it would use (0: unsupported), kr_out = K range per block.
 int gemv_splits(int M, int N, int K, int* kr_out);
 void gemv_set_target_blocks(int blocks);   // microbenchmark knob (default 256)
+void gemv_set_ablation(int bits);          // microbenchmark knob: LayerNorm-operand ablations (default 0)
 bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      size_t ws_bytes, hipStream_t st);
 // Whether the small-M path can run this shape as a residual producer with row statistics (EPI_RESID_F32 +

@@ -563,7 +563,8 @@ bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int
 // 16-column tiles x K splits, >= ~256 blocks (gemv_plan).
 template <int MF, int KSW, int KIND, bool LNA>
 __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
-                                                       int K, GemmEpi epi, int splitk, int kr, float* __restrict__ part) {
+                                                       int K, GemmEpi epi, int splitk, int kr, float* __restrict__ part,
+                                                       int abl) {
   __shared__ __attribute__((aligned(16))) f32x4 sred[4][MF][64];
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -605,11 +606,15 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
     const int m = min(lane & 15, M - 1);
     const float* xr = a.lnx + (long long)m * a.ld + kb + 8 * (lane >> 4);
     f32x4 xv[KSW][2];
+    const bool xon = !(abl & 2) || (lane & 15) < M;
 #pragma unroll
     for (int s = 0; s < KSW; ++s)
       if (s0 + s < s1) {
-        xv[s][0] = *(const f32x4*)(xr + 32 * (s0 + s));
-        xv[s][1] = *(const f32x4*)(xr + 32 * (s0 + s) + 4);
+        xv[s][0] = xv[s][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (xon) {
+          xv[s][0] = *(const f32x4*)(xr + 32 * (s0 + s));
+          xv[s][1] = *(const f32x4*)(xr + 32 * (s0 + s) + 4);
+        }
       }
     // every load first (one memory round trip with the weight stream): the block's affine range and this
     // thread's share of the row statistics -- thread t sums tiles [g T / 16, (g + 1) T / 16) of row t & 15
@@ -621,13 +626,14 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
     const int t0 = g * T / 16, t1 = (g + 1) * T / 16;
     float2 sv[TG];
 #pragma unroll
-    for (int j = 0; j < TG; ++j) sv[j] = *(const float2*)(a.ln_stat + ((long long)min(t0 + j, T - 1) * M + mr) * 2);
+    for (int j = 0; j < TG; ++j)
+      sv[j] = (abl & 1) ? make_float2(0.f, 1.f) : *(const float2*)(a.ln_stat + ((long long)min(t0 + j, T - 1) * M + mr) * 2);
     float gv[5], bv[5];                                      // klen <= 1280 = 5 x 256
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int i = min(tid + 256 * j, klen - 1);
-      gv[j] = a.ln_g[kb + i];
-      bv[j] = a.ln_b[kb + i];
+      gv[j] = (abl & 4) ? 1.f : a.ln_g[kb + i];
+      bv[j] = (abl & 4) ? 0.f : a.ln_b[kb + i];
     }
     {
       float q1 = 0.f;
@@ -644,11 +650,13 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
       }
     __syncthreads();
     float p1 = 0.f;
+    if (!(abl & 8)) {
 #pragma unroll
-    for (int g2 = 0; g2 < 16; ++g2) p1 += sst[g2][lane & 15][0];
+      for (int g2 = 0; g2 < 16; ++g2) p1 += sst[g2][lane & 15][0];
+    }
     const float invn = 1.0f / (float)(a.ln_tiles * 16);
     const float mean = p1 * invn;                            // row lane & 15 == row tid & 15 (this thread's tiles)
-    {
+    if (!(abl & 8)) {
       float q2 = 0.f;
 #pragma unroll
       for (int j = 0; j < TG; ++j)
@@ -657,11 +665,13 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
           q2 += sv[j].y + 16.0f * dm * dm;
         }
       sst[g][r16][1] = q2;
+      __syncthreads();
     }
-    __syncthreads();
-    float p2 = 0.f;
+    float p2 = (abl & 8) ? 1.f : 0.f;
+    if (!(abl & 8)) {
 #pragma unroll
-    for (int g2 = 0; g2 < 16; ++g2) p2 += sst[g2][lane & 15][1];
+      for (int g2 = 0; g2 < 16; ++g2) p2 += sst[g2][lane & 15][1];
+    }
     const float rstd = rsqrtf(p2 * invn + 1e-5f);
 #pragma unroll
     for (int s = 0; s < KSW; ++s)
@@ -741,6 +751,8 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
 // otherwise split K (ranges of a multiple of 128, <= 1280) until the grid reaches ~256 blocks.
 static int g_gemv_blocks = 256;          // target grid (tools/gemv_bench sweeps it: gemv_set_target_blocks)
 void gemv_set_target_blocks(int b) { g_gemv_blocks = b > 0 ? b : 256; }
+static int g_gemv_abl = 0;               // microbenchmark ablations of the LayerNorm operand (tools/gemv_bench only)
+void gemv_set_ablation(int b) { g_gemv_abl = b; }
 
 int gemv_splits(int M, int N, int K, int* kr_out) {
   if (M <= 0 || M > 32 || N % 16 != 0 || K % 128 != 0) return 0;
@@ -757,7 +769,7 @@ template <int MF, int KIND, bool LNA = false>
 static void run_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      int splitk, int kr, hipStream_t st) {
   hipLaunchKernelGGL((gemv_dec_kernel<MF, 10, KIND, LNA>), dim3((N / 16) * splitk), dim3(256), 0, st, a, w, ldw, M, N, K,
-                     epi, splitk, kr, ws);
+                     epi, splitk, kr, ws, g_gemv_abl);
   WM_LAUNCH_CHECK("gemv_dec_kernel");
 }
 
