@@ -238,7 +238,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   routes to f32 rounding.  "decode_gemv_ln" (default 1): passes of <= 16 rows compute the LayerNorms after the
  *   out and cout projections inside the cq / fc1 GEMMs (from the residual and the per-tile row sums and sums of
  *   squares about the tile means that the producers write: a two-pass-equivalent variance) instead of two combine
- *   launches per layer; agrees with the unfused form to f32 rounding.
+ *   launches per layer; agrees with the unfused form to f32 rounding.  "decode_gemv_ln_fc2" (default 0): 1 = also
+ *   fc2 writes the residual and its row statistics without split-K (16-wave blocks over K = 4 d) and the next layer's
+ *   qkv GEMM applies ln1 to its operand (one combine launch fewer per layer; measured ~5 % slower per decoder pass).
  *   "decode_ring_gemm" (default 1): 0 disables the all-rows ring GEMM (plan value 0 below falls back to the
  *   split-K skinny GEMM).
  *   "decode_gemm_plan" (default 1): preset routing of the six decoder projections (qkv, out, cq, cout, fc1, fc2)

@@ -32,9 +32,10 @@ def setup(request):
     return dims, eng, orc, enc, tok
 
 
-def _gen(eng, enc, tok, ws, beam, gemv, gemv_ln=1):
+def _gen(eng, enc, tok, ws, beam, gemv, gemv_ln=1, ln_fc2=0):
     eng.set_option("decode_gemv", gemv)
     eng.set_option("decode_gemv_ln", gemv_ln)
+    eng.set_option("decode_gemv_ln_fc2", ln_fc2)
     eng.set_option("cross_mode", 0 if beam > 1 else 1)
     try:
         eng.reserve(enc.shape[0], enc.shape[0] * beam)
@@ -44,6 +45,7 @@ def _gen(eng, enc, tok, ws, beam, gemv, gemv_ln=1):
     finally:
         eng.set_option("decode_gemv", 1)
         eng.set_option("decode_gemv_ln", 1)
+        eng.set_option("decode_gemv_ln_fc2", 0)
         eng.set_option("cross_mode", 1)
     return res
 
@@ -54,9 +56,11 @@ def test_gemv_route_vs_oracle_and_general_route(setup, ws, beam):
     a = _gen(eng, enc, tok, ws, beam, 1)
     b = _gen(eng, enc, tok, ws, beam, 0)
     c = _gen(eng, enc, tok, ws, beam, 1, gemv_ln=0)        # LayerNorm combine launches instead of the fused form
-    assert [r.tokens for r in a] == [r.tokens for r in b] == [r.tokens for r in c]
+    d = _gen(eng, enc, tok, ws, beam, 1, ln_fc2=1)         # opt-in: fc2 -> next layer's ln1 fused as well
+    assert [r.tokens for r in a] == [r.tokens for r in b] == [r.tokens for r in c] == [r.tokens for r in d]
     # the fused LayerNorm merges per-tile statistics (another summation order): f32-rounding agreement
     assert max(abs(x.score - y.score) for x, y in zip(a, c)) < 2e-3
+    assert max(abs(x.score - y.score) for x, y in zip(a, d)) < 2e-3
     encf = enc.float().cpu().numpy()
     opt = GenerateOptions(beam_size=beam, suppress_tokens=list(tok.suppressed_tokens([-1])), max_length=448)
     res = {w: r for w, r in zip(ws, a)}

@@ -183,6 +183,8 @@ struct wm_engine {
   int dec_graph = 1;         // decode steps replayed from one captured HIP graph (see generate)
   int dec_gemv = 1;          // passes of <= 32 rows: the small-M weight-streaming GEMM (gemm_dec.hip gemv)
   int dec_gemv_ln = 1;       // passes of <= 16 rows: the LayerNorms after out / cout computed inside cq / fc1
+  int dec_gemv_ln_fc2 = 0;   // ... and the one after fc2 inside the next layer's qkv (fc2 a 16-wave residual producer):
+                             // measured slower (fc2 on 80 blocks 11.5 us alone, as slab + combine; qkv +2.4 us)
   DevBuf d_lnstat;           // their per-(tile, row) partial row sums, one region per decode slice
   hipStream_t gst = nullptr; // the capture / replay stream (a graph cannot be captured on the legacy null stream)
   hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr;
@@ -584,13 +586,16 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     a.lnx = x; a.ln_g = g; a.ln_b = b; a.ln_stat = lnstat; a.ln_tiles = d / 16;
     return a;
   };
+  // fc2 -> the next layer's ln1 the same way: fc2 (K = 4d) writes the residual and its statistics without split-K,
+  // the next layer's qkv normalises its operand (the same for every layer of a pass, so layer l > 0's qkv knows)
+  const bool fc2_fuse = ln_fuse && e->dec_gemv_ln_fc2 && gemv_ln_fusable(rows, d, 4 * d, d);
   bf16* kc = skv + (size_t)(2 * l) * skv_layer;
   bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
   {
     GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, W.qkv_b);
     ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
     ep.d = d; ep.n_head = H; ep.head_dim = 64; ep.n_ctx = C;
-    gemm(DEC_QKV, amat(hb, d), W.qkv_w, d, 3 * d, d, ep);
+    gemm(DEC_QKV, (fc2_fuse && l > 0) ? ln_operand(W.ln1_w, W.ln1_b) : amat(hb, d), W.qkv_w, d, 3 * d, d, ep);
   }
   {
     ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
@@ -688,7 +693,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   }
   if (l + 1 < L) {
     const auto& Wn = dec_weights(e)[l + 1];
-    gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, resid_ln(Wn.ln1_w, Wn.ln1_b, W.fc2_b));
+    gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d,
+         fc2_fuse ? resid_stat(W.fc2_b) : resid_ln(Wn.ln1_w, Wn.ln1_b, W.fc2_b));
   } else {
     gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, epi_of(EPI_RESID_F32, x, d, W.fc2_b));
   }
@@ -2422,6 +2428,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "decode_graph") e->dec_graph = value != 0;
     else if (k == "decode_gemv") e->dec_gemv = value != 0;
     else if (k == "decode_gemv_ln") e->dec_gemv_ln = value != 0;
+    else if (k == "decode_gemv_ln_fc2") e->dec_gemv_ln_fc2 = value != 0;
     else if (k == "decode_ring_gemm") e->dec_ring = value != 0;
     else if (k == "decode_gemm_plan") {
       if (value != 0 && value != 1) throw std::runtime_error("wm_set_option: decode_gemm_plan is 0 or 1");
@@ -2496,6 +2503,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "decode_graph") *value = e->dec_graph;
     else if (k == "decode_gemv") *value = e->dec_gemv;
     else if (k == "decode_gemv_ln") *value = e->dec_gemv_ln;
+    else if (k == "decode_gemv_ln_fc2") *value = e->dec_gemv_ln_fc2;
     else if (k == "decode_ring_gemm") *value = e->dec_ring;
     else if (k == "decode_gemm_plan") {
       int p = -1;

@@ -560,12 +560,14 @@ bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int
 // (16x16x32: the weight fragment is the A operand, 16 columns x 32 k; the activations the B operand, 32 k x
 // 16 rows, MF fragments of 16 rows).  The 4 wave partials are summed through LDS in wave order, then the
 // epilogue runs in place (or a split-K slab is written: RESID_LN always, other kinds when kr < K).  Grid =
-// 16-column tiles x K splits, >= ~256 blocks (gemv_plan).
-template <int MF, int KSW, int KIND, bool LNA>
-__global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
-                                                       int K, GemmEpi epi, int splitk, int kr, float* __restrict__ part,
-                                                       int abl) {
-  __shared__ __attribute__((aligned(16))) f32x4 sred[4][MF][64];
+// 16-column tiles x K splits, >= ~256 blocks (gemv_plan).  NWV = 16 waves (1024 threads): a K range up to 5120 in
+// one block (fc2 as a residual producer with row statistics, no split-K), the 16 partials summed in wave order.
+template <int MF, int KSW, int KIND, bool LNA, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M,
+                                                            int N, int K, GemmEpi epi, int splitk, int kr,
+                                                            float* __restrict__ part, int abl) {
+  static_assert(!LNA || NWV == 4, "the LayerNorm operand's statistics split assumes 256 threads");
+  __shared__ __attribute__((aligned(16))) f32x4 sred[NWV][MF][64];
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -576,7 +578,7 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
   // guard the compiler treats as divergent runs anyway, on a skipped step's uninitialised operands: NaN outputs,
   // found by tools/gemv_check).  (Zeroing the operands instead costs a memory wait at the first guarded load.)
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int s0 = wv * nks / 4, s1 = (wv + 1) * nks / 4;
+  const int s0 = wv * nks / NWV, s1 = (wv + 1) * nks / NWV;
   const bf16* wr = w + (long long)min(n0 + (lane & 15), N - 1) * ldw + kb + 8 * (lane >> 4);
   bf16x8 fw[KSW], fa[KSW][MF];
 #pragma unroll
@@ -708,7 +710,9 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
     // the 4 of a lane, then the 4 lanes)
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
-      const f32x4 v = sred[0][i][lane] + sred[1][i][lane] + sred[2][i][lane] + sred[3][i][lane];
+      f32x4 v = sred[0][i][lane];
+#pragma unroll
+      for (int w2 = 1; w2 < NWV; ++w2) v += sred[w2][i][lane];
       const int row = i * 16 + (lane & 15);
       const bool ok = row < M && col0 < N;
       float q1 = 0.f, q2 = 0.f;
@@ -737,7 +741,9 @@ __global__ __launch_bounds__(256) void gemv_dec_kernel(GemmA a, const bf16* __re
   }
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
-    const f32x4 v = sred[0][i][lane] + sred[1][i][lane] + sred[2][i][lane] + sred[3][i][lane];
+    f32x4 v = sred[0][i][lane];
+#pragma unroll
+    for (int w2 = 1; w2 < NWV; ++w2) v += sred[w2][i][lane];
     const int row = i * 16 + (lane & 15);
     if (row >= M || col0 >= N) continue;
     if (to_slab)
@@ -765,11 +771,11 @@ int gemv_splits(int M, int N, int K, int* kr_out) {
   return s;
 }
 
-template <int MF, int KIND, bool LNA = false>
+template <int MF, int KIND, bool LNA = false, int NWV = 4>
 static void run_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      int splitk, int kr, hipStream_t st) {
-  hipLaunchKernelGGL((gemv_dec_kernel<MF, 10, KIND, LNA>), dim3((N / 16) * splitk), dim3(256), 0, st, a, w, ldw, M, N, K,
-                     epi, splitk, kr, ws, g_gemv_abl);
+  hipLaunchKernelGGL((gemv_dec_kernel<MF, 10, KIND, LNA, NWV>), dim3((N / 16) * splitk), dim3(NWV * 64), 0, st, a, w, ldw,
+                     M, N, K, epi, splitk, kr, ws, g_gemv_abl);
   WM_LAUNCH_CHECK("gemv_dec_kernel");
 }
 
@@ -781,13 +787,13 @@ static void dispatch_gemv(const GemmA& a, const bf16* w, long long ldw, int M, i
 }
 
 bool gemv_ln_fusable(int M, int N_prod, int K_prod, int K_cons) {
-  return M >= 1 && M <= 16 && N_prod % 16 == 0 && N_prod / 16 <= 128 && K_prod % 128 == 0 && K_prod <= 1280 &&
+  return M >= 1 && M <= 16 && N_prod % 16 == 0 && N_prod / 16 <= 128 && K_prod % 128 == 0 && K_prod <= 5120 &&
          K_cons == N_prod && K_cons % 128 == 0;
 }
 
 // Small-M path: M <= 32, N % 16 == 0, K % 128 == 0.  Returns false when unsupported.  A residual producer with
-// row statistics (EPI_RESID_F32 + stat_out) runs without split-K; a LayerNorm-consuming operand (a.lnx) is
-// supported for bf16 outputs at M <= 16.
+// row statistics (EPI_RESID_F32 + stat_out) runs without split-K (K > 1280, up to 5120: 16-wave blocks); a
+// LayerNorm-consuming operand (a.lnx) is supported for bf16 outputs and the self-attention qkv epilogue at M <= 16.
 bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      size_t ws_bytes, hipStream_t st) {
   int kr = 0;
@@ -795,21 +801,26 @@ bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if (splitk <= 0) return false;
   const bool stat = epi.kind == EPI_RESID_F32 && epi.stat_out;
   if (stat) {
-    if (M > 16 || K > 1280 || N / 16 > 128) return false;
+    if (M > 16 || K > 5120 || N / 16 > 128) return false;
     splitk = 1;
     kr = K;
   }
   if (a.lnx) {
-    if (epi.kind != EPI_BF16 || M > 16 || kr > 1280 || a.ln_tiles < 1 || a.ln_tiles > 128 || a.ld % 4 != 0 ||
-        a.ln_tiles * 16 != K)
+    if ((epi.kind != EPI_BF16 && epi.kind != EPI_DEC_QKV) || M > 16 || kr > 1280 || a.ln_tiles < 1 ||
+        a.ln_tiles > 128 || a.ld % 4 != 0 || a.ln_tiles * 16 != K)
       return false;
   }
   const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   if (a.lnx) {
-    run_gemv<1, EPI_BF16, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    if (epi.kind == EPI_DEC_QKV) run_gemv<1, EPI_DEC_QKV, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    else run_gemv<1, EPI_BF16, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
     if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
+    return true;
+  }
+  if (stat && K > 1280) {
+    run_gemv<1, EPI_RESID_F32, false, 16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
     return true;
   }
   switch (epi.kind) {
