@@ -581,10 +581,21 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
   const int s0 = wv * nks / NWV, s1 = (wv + 1) * nks / NWV;
   const bf16* wr = w + (long long)min(n0 + (lane & 15), N - 1) * ldw + kb + 8 * (lane >> 4);
   bf16x8 fw[KSW], fa[KSW][MF];
+  // (LNA: every step's load issued unconditionally, the step clamped into the block's range, so the load count is
+  // static and the statistics merge waits for its own loads only; the MFMAs keep their scalar step guards)
+  auto load_w = [&]() {
 #pragma unroll
-  for (int s = 0; s < KSW; ++s)
-    if (s0 + s < s1) fw[s] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const i32x4*)(wr + 32 * (s0 + s))));
+    for (int s = 0; s < KSW; ++s) {
+      if (LNA) {
+        const int sc = min(s0 + s, nks - 1);
+        fw[s] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const i32x4*)(wr + 32 * sc)));
+      } else if (s0 + s < s1) {
+        fw[s] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const i32x4*)(wr + 32 * (s0 + s))));
+      }
+    }
+  };
   if constexpr (!LNA) {
+    load_w();
     const bf16* ar[MF];
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
@@ -604,24 +615,15 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
     // sum of squares about the tile's own mean); then A = bf16((x - mean) * rstd * g + b).  The variance is
     // two-pass-equivalent: within-tile M2 plus 16 (tile mean - mean)^2 per tile, after the mean (no E[x^2] - mean^2
     // cancellation), so it agrees with resid_ln_reduce_kernel's two-pass statistics to f32 rounding.
+    // Load order: the statistics and the affine range first, then the weight stream, then the activations, and the
+    // barriers of the statistics merge are raw (LDS only: `s_waitcnt lgkmcnt(0); s_barrier`), so only the first
+    // loads must have landed when the merge runs; the weight and activation loads stay in flight behind it and
+    // each k-step waits for its own operands.  (With the loads issued weights-first and __syncthreads, whose
+    // workgroup fence waits for every outstanding load, the operand cost 2.1-3.1 us per launch over a bf16 one.)
     __shared__ __attribute__((aligned(16))) float sg[1280], sb[1280];
-    const int m = min(lane & 15, M - 1);
-    const float* xr = a.lnx + (long long)m * a.ld + kb + 8 * (lane >> 4);
-    f32x4 xv[KSW][2];
-    const bool xon = !(abl & 2) || (lane & 15) < M;
-#pragma unroll
-    for (int s = 0; s < KSW; ++s)
-      if (s0 + s < s1) {
-        xv[s][0] = xv[s][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (xon) {
-          xv[s][0] = *(const f32x4*)(xr + 32 * (s0 + s));
-          xv[s][1] = *(const f32x4*)(xr + 32 * (s0 + s) + 4);
-        }
-      }
-    // every load first (one memory round trip with the weight stream): the block's affine range and this
-    // thread's share of the row statistics -- thread t sums tiles [g T / 16, (g + 1) T / 16) of row t & 15
-    // (g = t >> 4, at most 8 tiles); the 16 group partials go through LDS and each lane adds them in group order
-    // (so every lane of a row, and every block, gets the same bits)
+    // thread t sums tiles [g T / 16, (g + 1) T / 16) of row t & 15 (g = t >> 4, at most 8 tiles); the 16 group
+    // partials go through LDS and each lane adds them in group order (so every lane of a row, and every block,
+    // gets the same bits)
     __shared__ float sst[16][16][2];
     constexpr int TG = 8;                                    // T <= 128 tiles (N <= 2048)
     const int T = a.ln_tiles, g = tid >> 4, r16 = tid & 15, mr = min(r16, M - 1);
@@ -637,6 +639,16 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
       gv[j] = (abl & 4) ? 1.f : a.ln_g[kb + i];
       bv[j] = (abl & 4) ? 0.f : a.ln_b[kb + i];
     }
+    load_w();
+    const int m = min(lane & 15, M - 1);
+    const float* xr = a.lnx + (long long)m * a.ld + kb + 8 * (lane >> 4);
+    f32x4 xv[KSW][2];
+#pragma unroll
+    for (int s = 0; s < KSW; ++s) {
+      const int sc = min(s0 + s, nks - 1);
+      xv[s][0] = *(const f32x4*)(xr + 32 * sc);
+      xv[s][1] = *(const f32x4*)(xr + 32 * sc + 4);
+    }
     {
       float q1 = 0.f;
 #pragma unroll
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
         sg[tid + 256 * j] = gv[j];
         sb[tid + 256 * j] = bv[j];
       }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     float p1 = 0.f;
     if (!(abl & 8)) {
 #pragma unroll
@@ -667,7 +679,7 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
           q2 += sv[j].y + 16.0f * dm * dm;
         }
       sst[g][r16][1] = q2;
-      __syncthreads();
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     float p2 = (abl & 8) ? 1.f : 0.f;
     if (!(abl & 8)) {
@@ -771,12 +783,23 @@ int gemv_splits(int M, int N, int K, int* kr_out) {
   return s;
 }
 
-template <int MF, int KIND, bool LNA = false, int NWV = 4>
+template <int MF, int KIND, bool LNA = false, int NWV = 4, int KSW = 10>
 static void run_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      int splitk, int kr, hipStream_t st) {
-  hipLaunchKernelGGL((gemv_dec_kernel<MF, 10, KIND, LNA, NWV>), dim3((N / 16) * splitk), dim3(NWV * 64), 0, st, a, w, ldw,
-                     M, N, K, epi, splitk, kr, ws, g_gemv_abl);
+  hipLaunchKernelGGL((gemv_dec_kernel<MF, KSW, KIND, LNA, NWV>), dim3((N / 16) * splitk), dim3(NWV * 64), 0, st, a, w,
+                     ldw, M, N, K, epi, splitk, kr, ws, g_gemv_abl);
   WM_LAUNCH_CHECK("gemv_dec_kernel");
+}
+
+// The LayerNorm-operand form issues every one of its KSW steps' loads (clamped, so the count is static): KSW is
+// the per-wave step count of this K range rounded up to 3, 5 or 10 (cq at 4 K splits: 3 steps, not 10 loads)
+template <int KIND>
+static void run_gemv_lna(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                         int splitk, int kr, hipStream_t st) {
+  const int per_wave = (kr / 32 + 3) / 4;
+  if (per_wave <= 3) run_gemv<1, KIND, true, 4, 3>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else if (per_wave <= 5) run_gemv<1, KIND, true, 4, 5>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  else run_gemv<1, KIND, true, 4, 10>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
 template <int KIND>
@@ -814,8 +837,8 @@ bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   if (a.lnx) {
-    if (epi.kind == EPI_DEC_QKV) run_gemv<1, EPI_DEC_QKV, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-    else run_gemv<1, EPI_BF16, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    if (epi.kind == EPI_DEC_QKV) run_gemv_lna<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    else run_gemv_lna<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
     if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
     return true;
   }
