@@ -1144,10 +1144,12 @@ void launch_cross_attn(const bf16* q, long long ldq, const bf16* kbase, const bf
     const int ntt = (T + 63) / 64;
     int splits = 1;
     if (mf_dec) {
-      // key splits until ~2 rounds of blocks fill the chip; a function of the whole pass (plan_rows), so a row's
-      // summation order does not depend on how the pass is sliced
+      // key splits until ~one round of blocks fills the chip (256 blocks: at one window, 13 splits of ~2 tiles; a
+      // 512-block target, 16 splits, measured 4 % slower: 109 vs 104-105 ms of cross-attention per 60 s beam-5 call,
+      // `prof_worker_seq_r04_tf_target_ab.jsonl`); a function of the whole pass (plan_rows), so a row's summation
+      // order does not depend on how the pass is sliced
       const int plan_blocks = plan_rows / group * H * nqt;
-      splits = std::max(1, std::min(std::min(16, ntt), (512 + plan_blocks - 1) / plan_blocks));
+      splits = std::max(1, std::min(std::min(16, ntt), (256 + plan_blocks - 1) / plan_blocks));
     }
     a.splits = splits;
     // in-kernel combine only for decode key splits (one row tile per group: the counters are rows/group x H)
