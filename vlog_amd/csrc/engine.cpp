@@ -202,6 +202,9 @@ struct wm_engine {
                              // costs ~3 round trips, more than the combine kernel behind it in the stream)
   int dec_big_rows = 320;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
                              // whole K per block (decoder_layer)
+  int dec_big_lds = 72;      // ... with this LDS budget per ring block (KiB): 72 = two resident blocks per CU
+                             // (tools/dec_gemm_bench at 750 rows: qkv 24.7 -> 18.8 us, fc1 31.3 -> 21.4, fc2 41.6 -> 33.1
+                             // against 144; bit-identical: the ring depth never changes a row's K order)
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
                              // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
@@ -556,7 +559,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
     const int kr = e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 || big ? K : 1280);
-    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols)) return;
+    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols, big ? e->dec_big_lds : 0)) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
     launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
@@ -2159,6 +2162,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_XSNAKE")) e->xsnake = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_XKEEP")) e->xkeep = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_LDS")) e->dec_big_lds = std::atoi(v) == 144 ? 144 : 72;
     try {
       build_layout(e);
       build_frontend(e, nullptr);
@@ -2485,6 +2489,10 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_mfma") e->cross_mfma = value ? 1 : 0;
     else if (k == "cross_mfma_fuse") e->cross_mfma_fuse = value ? 1 : 0;
     else if (k == "decode_gemm_big_rows") e->dec_big_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
+    else if (k == "decode_gemm_big_lds") {
+      if (value != 72 && value != 144) throw std::runtime_error("decode_gemm_big_lds: 72 or 144");
+      e->dec_big_lds = (int)value;
+    }
     else throw std::runtime_error("wm_set_option: unknown option " + k);
   });
 }
@@ -2528,6 +2536,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_mfma") *value = e->cross_mfma;
     else if (k == "cross_mfma_fuse") *value = e->cross_mfma_fuse;
     else if (k == "decode_gemm_big_rows") *value = e->dec_big_rows;
+    else if (k == "decode_gemm_big_lds") *value = e->dec_big_lds;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
   });
 }

@@ -78,9 +78,10 @@ bool launch_dec_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N,
 void launch_splitk_combine(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st);
 // Ring-pipelined decoder-row path (gemm_dec.hip): M <= 160; kr = K range per block (0 = whole K up to 1280).
 // rows_per_block > 0: the rows are split into groups of that many (32..160) — one block per (32-column tile, row
-// group, K split); the row groups of a tile share its weight panel through one XCD's L2 (any M).
+// group, K split); the row groups of a tile share its weight panel through one XCD's L2 (any M).  lds_kb: the ring's
+// LDS budget, 144 (one block per CU) or 72 (two resident blocks per CU); 0 = the process default (VLOG_AMD_RING_LDS).
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block = 0, int cols = 32);
+                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block = 0, int cols = 32, int lds_kb = 0);
 // One-shot decoder-row path (gemm_dec.hip): 32 rows x nc*16 columns per 512-thread block, every load of a
 // <= 1280-deep K range issued at once into MFMA operand registers, per-wave K split summed through LDS.
 bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,

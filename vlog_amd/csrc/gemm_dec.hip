@@ -348,8 +348,8 @@ static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, in
 
 template <int MF, int KIND, int NC>
 static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     int splitk, int kr, hipStream_t st) {
-  if (ring_lds_kb() == 72) run_ring_cap<MF, KIND, NC, 72>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+                     int splitk, int kr, hipStream_t st, int lds_kb) {
+  if ((lds_kb > 0 ? lds_kb : ring_lds_kb()) == 72) run_ring_cap<MF, KIND, NC, 72>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
   else run_ring_cap<MF, KIND, NC, 144>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
@@ -357,19 +357,19 @@ static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
 // and ceil(M / rows) row groups.
 template <int KIND>
 static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
-                          float* ws, int splitk, int kr, int rows_per_block, int cols, hipStream_t st) {
+                          float* ws, int splitk, int kr, int rows_per_block, int cols, hipStream_t st, int lds_kb) {
   const int rows = rows_per_block > 0 ? std::min(rows_per_block, ((M + 31) / 32) * 32) : M;
   if (cols == 64) {                      // 64-column tiles: row groups of <= 64 (the ring slot must hold 3 x 2 sub-panels)
-    if (rows <= 32) run_ring<2, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-    else if (rows <= 64) run_ring<4, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+    if (rows <= 32) run_ring<2, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+    else if (rows <= 64) run_ring<4, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
     else throw std::runtime_error("dec_ring: 64-column tiles take at most 64 rows per block");
     return;
   }
-  if (rows <= 32) run_ring<2, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (rows <= 64) run_ring<4, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (rows <= 96) run_ring<6, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else if (rows <= 128) run_ring<8, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else run_ring<10, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+  if (rows <= 32) run_ring<2, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+  else if (rows <= 64) run_ring<4, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+  else if (rows <= 96) run_ring<6, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+  else if (rows <= 128) run_ring<8, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+  else run_ring<10, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
 }
 
 // Ring path: N % 4 == 0, K % 64 == 0; M <= 160 for one row group, any M with rows_per_block > 0.  kr = K range
@@ -377,7 +377,8 @@ static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, i
 // 32 or 64 (64: at most 64 rows per block).  A column tile's width never changes a row's K summation order, so
 // both widths give bit-identical results.  Returns false when unsupported.
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block, int cols) {
+                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block, int cols, int lds_kb) {
+  if (lds_kb != 0 && lds_kb != 72 && lds_kb != 144) return false;
   if ((rows_per_block <= 0 && M > 160) || rows_per_block > 160 || N % 4 != 0 || K % 64 != 0) return false;
   if (cols != 32 && cols != 64) return false;
   if (cols == 64 && (rows_per_block <= 0 ? M : std::min(rows_per_block, ((M + 31) / 32) * 32)) > 64) return false;
@@ -389,11 +390,11 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   switch (epi.kind) {
-    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
-    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
-    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
-    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
-    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st); break;
+    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
+    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
+    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
+    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
+    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
     default: return false;
   }
   if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
