@@ -251,11 +251,11 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_gemm_cols.<proj>" (preset 1: 64 for fc1 and fc2, else 32): output columns per ring-GEMM block, 32 or 64 (64
  *   takes row groups of at most 64; other routes ignore it).  Bit-identical either way.  decode_gemm_plan also
  *   resets these to its preset.
- *   "decode_gemm_big_rows" (default 320): passes of at least this many rows (<= 1024; beam groups of many windows)
- *   route every projection to 64-row ring groups over its whole K (64 columns for qkv / fc1, and for all from 512
- *   rows; 0 disables).  Results agree to f32 rounding.
- *   "decode_gemm_big_lds" (default 72): LDS budget in KiB of those ring blocks, 72 (two resident blocks per CU) or 144
- *   (one).  Bit-identical either way.
+ *   "decode_gemm_big_rows" (default 161): passes of at least this many rows (<= 1024; beam groups of many windows)
+ *   route every projection to 64-row ring groups over its whole K (64 columns for qkv / fc1 / fc2, and for all from
+ *   512 rows; 0 disables).  Results agree to f32 rounding.
+ *   "decode_gemm_big_lds" (default 72): LDS budget in KiB of the qkv / fc1 / fc2 ring blocks on that route, 72 (two
+ *   resident blocks per CU) or 144 (one; the d x d projections always take 144).  Bit-identical either way.
  *   "gemm_persistent" (default 0, process-wide): 1 runs large encoder GEMMs as one persistent block per CU
  *   walking its tiles, the next tile's first K-tiles loaded during the current tile's last K-steps and epilogue
  *   (measured no faster than one block per tile).  Bit-identical.

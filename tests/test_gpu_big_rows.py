@@ -1,7 +1,8 @@
 """Decoder passes of >= decode_gemm_big_rows rows (beam groups of many windows; engine.cpp decoder_layer): the
 64-row ring-GEMM route at its two LDS budgets ("decode_gemm_big_lds" 72 = two resident blocks per CU, the default,
 and 144 = one) must give the same bits — the ring depth never changes a row's K summation order — and the same
-tokens as the route below the threshold.  Beam 5 over 64 windows of the margin-planted tiny model: 320 rows."""
+tokens as the route below the threshold.  Beam 5 over 64 windows of the margin-planted tiny model: 320 rows (and
+over 40 windows: 200 rows, above the default threshold of 161 since the 64 x 64 two-blocks-per-CU tiles)."""
 import numpy as np
 import pytest
 import torch
@@ -27,7 +28,7 @@ def setup():
     return dims, eng, enc, Tokenizer(dims, language="en")
 
 
-def _beam(eng, enc, tok, **opts):
+def _beam(eng, enc, tok, n=W, **opts):
     old = {k: eng.option(k) for k in opts}
     for k, v in opts.items():
         eng.set_option(k, v)
@@ -35,7 +36,7 @@ def _beam(eng, enc, tok, **opts):
     try:
         eng.reserve(W, W * 5)
         eng.cross_kv(enc, 0)
-        res, _ = eng.generate(list(range(W)), [list(tok.sot_sequence)] * W, beam_size=5,
+        res, _ = eng.generate(list(range(n)), [list(tok.sot_sequence)] * n, beam_size=5,
                               suppress_tokens=list(tok.suppressed_tokens([-1])), max_length=448)
     finally:
         for k, v in old.items():
@@ -46,7 +47,7 @@ def _beam(eng, enc, tok, **opts):
 
 def test_big_rows_lds_budgets_bit_identical(setup):
     dims, eng, enc, tok = setup
-    assert eng.option("decode_gemm_big_lds") == 72 and eng.option("decode_gemm_big_rows") == 320
+    assert eng.option("decode_gemm_big_lds") == 72 and eng.option("decode_gemm_big_rows") == 161
     a = _beam(eng, enc, tok, decode_gemm_big_lds=72)
     b = _beam(eng, enc, tok, decode_gemm_big_lds=144)
     c = _beam(eng, enc, tok, decode_gemm_big_rows=0)            # the route below the threshold
@@ -54,6 +55,10 @@ def test_big_rows_lds_budgets_bit_identical(setup):
     assert [r.score for r in a] == [r.score for r in b]         # bit for bit
     assert [r.tokens for r in a] == [r.tokens for r in c]
     assert max(abs(x.score - y.score) for x, y in zip(a, c)) < 2e-3
+    d = _beam(eng, enc, tok, n=40)                                # 200 rows
+    e = _beam(eng, enc, tok, n=40, decode_gemm_big_rows=0)
+    assert [r.tokens for r in d] == [r.tokens for r in e] == [r.tokens for r in a[:40]]
+    assert max(abs(x.score - y.score) for x, y in zip(d, e)) < 2e-3
 
 
 def test_big_lds_option_validation(setup):

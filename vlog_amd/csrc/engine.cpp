@@ -200,11 +200,12 @@ struct wm_engine {
   int cross_mfma_fuse = 0;   // ... its key-split combine done by the last-arriving split (d_cross_cnt), not a kernel:
                              // measured slower (16.3 vs 15.3 us per layer at 1 window, beam 5: the L2 hand-off
                              // costs ~3 round trips, more than the combine kernel behind it in the stream)
-  int dec_big_rows = 320;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
-                             // whole K per block (decoder_layer)
-  int dec_big_lds = 72;      // ... with this LDS budget per ring block (KiB): 72 = two resident blocks per CU
-                             // (tools/dec_gemm_bench at 750 rows: qkv 24.7 -> 18.8 us, fc1 31.3 -> 21.4, fc2 41.6 -> 33.1
-                             // against 144; bit-identical: the ring depth never changes a row's K order)
+  int dec_big_rows = 161;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
+                             // whole K per block (decoder_layer); 320 before the two-blocks-per-CU tiles below
+  int dec_big_lds = 72;      // ... qkv / fc1 / fc2 with this LDS budget per ring block (KiB): 72 = two resident blocks
+                             // per CU (tools/dec_gemm_bench at 750 rows: qkv 24.7 -> 18.8 us, fc1 31.3 -> 21.4, fc2
+                             // 41.6 -> 33.1 against 144; at 256 rows qkv+fc1+fc2 45.6 -> 35.7 us per layer against the
+                             // 150-row plan; bit-identical: the ring depth never changes a row's K order)
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
                              // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
@@ -555,11 +556,16 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     const int tr = sl.total_rows;
     const bool big = e->dec_big_rows > 0 && tr >= e->dec_big_rows && tr <= 1024;
     const int p = big ? 64 : plan_of(proj);
-    const int cols = big ? ((tr >= 512 || proj == DEC_QKV || proj == DEC_FC1) ? 64 : 32) : e->dec_cols[proj];
+    // the three d x d projections keep 32-column tiles below 512 rows and one block per CU (144 KiB); qkv / fc1 / fc2
+    // take 64 x 64 tiles, two blocks per CU (dec_big_lds; tools/dec_gemm_bench at 256 / 384 / 750 rows,
+    // profiles/dec_gemm_bench_r04_*rows_lds*.txt)
+    const bool sq = proj == DEC_OUT || proj == DEC_CQ || proj == DEC_COUT;
+    const int cols = big ? ((tr >= 512 || !sq) ? 64 : 32) : e->dec_cols[proj];
+    const int lds = big ? (sq ? 144 : e->dec_big_lds) : 0;
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
     const int kr = e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 || big ? K : 1280);
-    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols, big ? e->dec_big_lds : 0)) return;
+    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols, lds)) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
     launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
@@ -2163,6 +2169,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_XKEEP")) e->xkeep = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_LDS")) e->dec_big_lds = std::atoi(v) == 144 ? 144 : 72;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_ROWS")) e->dec_big_rows = std::max(0, std::atoi(v));
     try {
       build_layout(e);
       build_frontend(e, nullptr);
