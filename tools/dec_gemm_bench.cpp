@@ -152,9 +152,9 @@ int main(int argc, char** argv) {
     for (int pad : {0, 64}) {
       // pad: activation row stride K + pad (a 64-element pad moves consecutive rows to different L2 channels)
       const GemmA ap{dA, (long long)s.K + pad, 0, 0};
-      for (int rpb : {0, 32, 64, 96})
+      for (int rpb : {0, 32, 64, 96, 128})
       for (int cols : {32, 64}) {
-        if (cols == 64 && (pad || rpb == 0 || rpb > 64)) continue;
+        if (cols == 64 && (pad || rpb == 0 || rpb == 96)) continue;
         for (int kr : {0, 640, 1280, 2560, 5120}) {
           if (kr > s.K || (kr > 0 && kr != s.K && s.K <= 1280)) continue;
           if (pad && kr != 0) continue;

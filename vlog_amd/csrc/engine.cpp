@@ -202,6 +202,9 @@ struct wm_engine {
                              // costs ~3 round trips, more than the combine kernel behind it in the stream)
   int dec_big_rows = 161;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
                              // whole K per block (decoder_layer); 320 before the two-blocks-per-CU tiles below
+  int dec_big128 = 0;        // ... from this many rows qkv / fc1 / fc2 in 128-row groups (0: never; VLOG_AMD_DEC_BIG128).
+                             // Off: faster alone (dec_gemm_bench, 750 rows) but slower in the step (config 5, arms
+                             // alternating on one box: dec_gemm 605 vs 566 ms per step, profiles/ab_r04_c5_big128.txt)
   int dec_big_lds = 72;      // ... qkv / fc1 / fc2 with this LDS budget per ring block (KiB): 72 = two resident blocks
                              // per CU (tools/dec_gemm_bench at 750 rows: qkv 24.7 -> 18.8 us, fc1 31.3 -> 21.4, fc2
                              // 41.6 -> 33.1 against 144; at 256 rows qkv+fc1+fc2 45.6 -> 35.7 us per layer against the
@@ -555,11 +558,13 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     // (384 rows: 76 vs 86 us per layer for the 150-row plan; 750 rows: 114 vs 159 us)
     const int tr = sl.total_rows;
     const bool big = e->dec_big_rows > 0 && tr >= e->dec_big_rows && tr <= 1024;
-    const int p = big ? 64 : plan_of(proj);
+    // (opt-in dec_big128: qkv / fc1 / fc2 in 128-row groups, 750 rows two blocks per CU 17.2 / 18.4 / 25.6 us against
+    // 18.9 / 21.0 / 32.8 for 64-row groups in tools/dec_gemm_bench, yet slower inside the decode step)
+    const bool sq = proj == DEC_OUT || proj == DEC_CQ || proj == DEC_COUT;
+    const int p = big ? ((e->dec_big128 > 0 && tr >= e->dec_big128 && !sq) ? 128 : 64) : plan_of(proj);
     // the three d x d projections keep 32-column tiles below 512 rows and one block per CU (144 KiB); qkv / fc1 / fc2
     // take 64 x 64 tiles, two blocks per CU (dec_big_lds; tools/dec_gemm_bench at 256 / 384 / 750 rows,
     // profiles/dec_gemm_bench_r04_*rows_lds*.txt)
-    const bool sq = proj == DEC_OUT || proj == DEC_CQ || proj == DEC_COUT;
     const int cols = big ? ((tr >= 512 || !sq) ? 64 : 32) : e->dec_cols[proj];
     const int lds = big ? (sq ? 144 : e->dec_big_lds) : 0;
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
@@ -2170,6 +2175,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_LDS")) e->dec_big_lds = std::atoi(v) == 144 ? 144 : 72;
     if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_ROWS")) e->dec_big_rows = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("VLOG_AMD_DEC_BIG128")) e->dec_big128 = std::max(0, std::atoi(v));
     try {
       build_layout(e);
       build_frontend(e, nullptr);

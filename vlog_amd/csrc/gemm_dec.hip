@@ -359,10 +359,11 @@ template <int KIND>
 static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
                           float* ws, int splitk, int kr, int rows_per_block, int cols, hipStream_t st, int lds_kb) {
   const int rows = rows_per_block > 0 ? std::min(rows_per_block, ((M + 31) / 32) * 32) : M;
-  if (cols == 64) {                      // 64-column tiles: row groups of <= 64 (the ring slot must hold 3 x 2 sub-panels)
+  if (cols == 64) {                      // 64-column tiles: row groups of 32, 64 or 128
     if (rows <= 32) run_ring<2, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
     else if (rows <= 64) run_ring<4, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
-    else throw std::runtime_error("dec_ring: 64-column tiles take at most 64 rows per block");
+    else if (rows <= 128) run_ring<8, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+    else throw std::runtime_error("dec_ring: 64-column tiles take at most 128 rows per block");
     return;
   }
   if (rows <= 32) run_ring<2, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
@@ -381,7 +382,7 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if (lds_kb != 0 && lds_kb != 72 && lds_kb != 144) return false;
   if ((rows_per_block <= 0 && M > 160) || rows_per_block > 160 || N % 4 != 0 || K % 64 != 0) return false;
   if (cols != 32 && cols != 64) return false;
-  if (cols == 64 && (rows_per_block <= 0 ? M : std::min(rows_per_block, ((M + 31) / 32) * 32)) > 64) return false;
+  if (cols == 64 && (rows_per_block <= 0 ? M : std::min(rows_per_block, ((M + 31) / 32) * 32)) > 128) return false;
   if (kr <= 0) kr = K <= 1280 ? K : ((K + (K + 1279) / 1280 - 1) / ((K + 1279) / 1280) + 63) / 64 * 64;
   if (kr % 64 != 0) return false;
   const int splitk = (K + kr - 1) / kr;
