@@ -11,6 +11,10 @@ offline) with a decisive, audio-dependent decoder program planted (vlog_amd/weig
 per window, segment boundaries every ~3.5 s), so the north_star parity gates can be checked on the bench's own
 windows (the `parity` block); the JSON reports the actual tokens per window.
 
+The default 1-GPU run appends a `variable` block to the same line: the realistic workload (plant margin_var: each
+window's audio sets its transcript length, so windows end at different steps), 150 windows through the row-set
+decode, timed the same way with its own roofline, decoder steps and active-row fraction (variable_block).
+
 Prints ONE JSON line on rank 0.  `python bench.py` (N=1) or torch.distributed.run --nproc-per-node N.
 """
 from __future__ import annotations
@@ -410,6 +414,139 @@ def cpu_baseline(dims, sd, mean_tokens: float, n_positions: int = 4):
                        f"unavailable (not installed)")}
 
 
+def roofline_block(breakdown, prof, dom, args, beam: int = 1, traffic_json: Optional[str] = None) -> dict:
+    """kernels_one_step, roofline (the dominant single-kernel class over the timed region), encoder_mfma and
+    decoder_kv_read from the engine's event profiler."""
+    out = {}
+    kern = {}
+    for k, v in breakdown.items():
+        if v["launches"] == 0:
+            continue
+        kern[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
+                   "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["flops"] else None,
+                   "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["bytes"] else None}
+    out["kernels_one_step"] = kern
+    v = prof[dom]                          # measured over the timed region
+    if dom in ("cross_attn", "self_attn", "select", "dec_other", "logmel") or (v["flops"] == 0):
+        ach = v["bytes"] / (v["ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4)}
+    else:
+        ach = v["flops"] / (v["ms"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(ach / MFMA_BF16_PEAK_TFS, 4)}
+    roof["kernel"] = dom
+    roof["launches"] = v["launches"]
+    roof["avg_launch_us"] = round(1000.0 * v["ms"] / max(v["launches"], 1), 2)
+    roof["traffic"] = None
+    tj_path = args.traffic_json if traffic_json is None else traffic_json
+    if tj_path and os.path.isfile(tj_path):
+        try:
+            tj = json.load(open(tj_path))
+            roof["traffic"] = tj.get(dom)
+        except Exception:
+            pass
+    if beam > 1 and not args.cross_fp8:
+        roof["accounting"] = ("projected cross-attention (beam groups): algorithmic bytes = each active window's "
+                              "K and V panels (L x 2 x 1500 x d bf16) per launch, counted in-kernel")
+    else:
+        roof["accounting"] = ("factored cross-attention: algorithmic bytes = each active window's encoder output "
+                              + ("(L x 1500 x d e4m3 + 1500 f32 scales)" if args.cross_fp8 else "(L x 1500 x d bf16)")
+                              + " + q' per launch, counted in-kernel")
+    out["roofline"] = roof
+    enc_ms = sum(breakdown[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
+    enc_fl = sum(breakdown[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
+    out["encoder_mfma"] = {"achieved_tflops": round(enc_fl / max(enc_ms, 1e-9) / 1e9, 1),
+                           "frac_of_2500": round(enc_fl / max(enc_ms, 1e-9) / 1e9 / MFMA_BF16_PEAK_TFS, 4)}
+    cx = breakdown["cross_attn"]
+    out["decoder_kv_read"] = {"achieved_gbs": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6, 1),
+                              "frac_of_8000": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6 / HBM_PEAK_GBS, 4)}
+    return out
+
+
+def timed_run(pipe, eng, steps: int, warmup: int, barrier, profile: bool = True, stream: bool = False):
+    """W untimed warmup steps, one untimed step with every kernel class under events (the breakdown and the
+    dominant single-kernel class), then exactly `steps` timed steps (events on the dominant class only), bracketed
+    by the barrier.  -> (elapsed s, breakdown, timed-region profile, dominant class, stage times of the timed steps)"""
+    for _ in range(warmup):
+        pipe.step()
+    breakdown, dom = None, None
+    if profile:
+        barrier()
+        eng.profile(True)
+        pipe.step()
+        eng.profile(False)
+        breakdown = eng.profile_read()
+        # the roofline names ONE kernel (it must match one rocprof row): classes that group several kernel
+        # variants (the GEMM families, combines, misc) are not candidates.  Events around the 27k decoder-GEMM
+        # launches per step would also slow the timed region.
+        single = {k: v for k, v in breakdown.items() if k in SINGLE_KERNEL_CLASSES and v["launches"]}
+        dom = max(single or breakdown, key=lambda k: (single or breakdown)[k]["ms"])
+    pipe.stage = {}
+    barrier()
+    if dom is not None:                       # timed region: events on the dominant class only
+        eng.profile(True, classes=[dom])
+    t0 = time.perf_counter()
+    if stream:
+        pipe.run_stream(steps)
+    else:
+        for _ in range(steps):
+            pipe.step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = None
+    if dom is not None:
+        eng.profile(False)
+        prof = eng.profile_read()
+    return elapsed, breakdown, prof, dom, dict(pipe.stage)
+
+
+def variable_block(args, dims, base_sd, tok, local: int, steps: int, warmup: int = 1) -> dict:
+    """The realistic workload in the same run: the margin_var plant (a window's audio sets where
+    its script ends, so windows decode different numbers of tokens), 150 windows of the same corpus, the row-set
+    decode (max_rows 0: all windows in flight, longest-expected first, finished rows compacted) -- the product's
+    throughput-mode schedule.  Timed exactly like the headline, on a fresh engine; no parity sample (the variable
+    gates run in tests/test_gpu_gates.py)."""
+    from vlog_amd.engine import GpuEngine
+    from vlog_amd.weights import plant_margin
+    t = time.perf_counter()
+    plant_margin(base_sd, dims, 0, variable=True)
+    eng = GpuEngine(dims, base_sd, local)
+    W = args.windows
+    pcm, margin = build_shard(0, W)
+    pcm_dev = torch.from_numpy(pcm).to(eng.device)
+    eng.reserve(W, W)
+    pipe = Pipeline(eng, tok, dims, 0, 1, W, 1, pcm_dev, margin, W * CLIP, None, check_every=args.check_every,
+                    g0=0, max_rows=0)
+    setup = time.perf_counter() - t
+    elapsed, breakdown, prof, dom, stage = timed_run(pipe, eng, steps, warmup, lambda: torch.cuda.synchronize(eng.device),
+                                                     profile=not args.no_profile)
+    toks = pipe.last["tokens"]
+    gs = pipe.last["gen_stats"]
+    blk = {"workload": "variable (weights.py plant margin_var; row-set decode, max_rows 0, longest-expected first, "
+                       "compaction)",
+           "value": round(W * 30.0 * steps / elapsed, 2), "unit": "audio_s/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": round(1000 * elapsed / steps, 2), "windows": W, "setup_s": round(setup, 1),
+           "mean_tokens_per_window": round(float(np.mean(toks)), 1),
+           "token_length_min_p50_max": [int(np.min(toks)), int(np.median(toks)), int(np.max(toks))],
+           "decoder_steps": pipe.last["steps"], "decoder_row_steps": gs.get("row_steps"),
+           "decoder_passes": gs.get("passes"),
+           "active_row_fraction": (round(sum(n + 1 for n in toks) / gs["row_steps"], 4) if gs.get("row_steps") else None),
+           "token_crc32": pipe.last["crc"],
+           "stages_s_per_step": {k: round(v / steps, 4) for k, v in stage.items()}}
+    if prof:
+        rb = roofline_block(breakdown, prof, dom, args, traffic_json="")
+        blk["roofline"] = rb["roofline"]
+        blk["encoder_mfma"] = rb["encoder_mfma"]
+        blk["decoder_kv_read"] = rb["decoder_kv_read"]
+        blk["kernels_one_step"] = rb["kernels_one_step"]
+    blk.setdefault("roofline", {})["composite"] = composite_roofline(dims, toks, pipe.last["steps"], len(pipe.prompt),
+                                                                   elapsed / steps, W)
+    del pipe, eng, pcm_dev
+    torch.cuda.empty_cache()
+    return blk
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -443,6 +580,10 @@ def main():
                          "finished windows' rows refilled from the next batch; ms_per_step = total / steps")
     ap.add_argument("--balance", choices=("count", "tokens"), default=None,
                     help="N > 1: windows per GPU by count, or by expected tokens (default for --workload variable)")
+    ap.add_argument("--no-variable", action="store_true",
+                    help="skip the variable-length block the default (uniform, 1 GPU) run appends to its line")
+    ap.add_argument("--variable-steps", type=int, default=None, help="timed steps of the variable block (default "
+                    "max(2, steps // 4))")
     args = ap.parse_args()
     if args.max_rows is None:
         args.max_rows = 0 if args.workload == "variable" else -1
@@ -481,8 +622,20 @@ def main():
     dims = model_dims(args.model)
     t = time.perf_counter()
     plant = "margin_var" if args.workload == "variable" else "margin"
-    sd = (synthetic_state_dict(dims, seed=0, eot_after=args.eot_after) if args.random_weights
-          else synthetic_state_dict(dims, seed=0, plant=plant))
+    # the default 1-GPU line also times the variable-length workload (variable_block) on a second engine
+    run_var = (world == 1 and args.workload == "uniform" and args.beam == 1 and not args.stream and not args.cross_fp8
+               and not args.random_weights and not args.no_variable and args.max_rows < 0 and dims.n_dec_layer >= 4)
+    base_sd = None
+    if args.random_weights:
+        sd = synthetic_state_dict(dims, seed=0, eot_after=args.eot_after)
+    elif run_var:
+        # one seeded random-init draw, planted twice (per-tensor generators: identical to generating each plant)
+        from vlog_amd.weights import plant_margin
+        base_sd = synthetic_state_dict(dims, seed=0)
+        sd = {k: v.clone() for k, v in base_sd.items()}
+        plant_margin(sd, dims, 0, variable=False)
+    else:
+        sd = synthetic_state_dict(dims, seed=0, plant=plant)
     from vlog_amd.engine import GpuEngine
     eng = GpuEngine(dims, sd, local)
     if args.cross_fp8:
@@ -528,37 +681,8 @@ def main():
             import torch.distributed as dist
             dist.barrier(group=host_group)
 
-    for _ in range(args.warmup):
-        pipe.step()
-    # one untimed step with every kernel class under events: the per-class breakdown and the dominant class
-    breakdown, dom = None, None
-    if not args.no_profile:
-        barrier()
-        eng.profile(True)
-        pipe.step()
-        eng.profile(False)
-        breakdown = eng.profile_read()
-        # the roofline names ONE kernel (it must match one rocprof row): classes that group several kernel
-        # variants (the GEMM families, combines, misc) are not candidates.  Events around the 27k decoder-GEMM
-        # launches per step would also slow the timed region.
-        single = {k: v for k, v in breakdown.items() if k in SINGLE_KERNEL_CLASSES and v["launches"]}
-        dom = max(single or breakdown, key=lambda k: (single or breakdown)[k]["ms"])
-    pipe.stage = {}
-    barrier()
-    if dom is not None:                       # timed region: events on the dominant class only
-        eng.profile(True, classes=[dom])
-    t0 = time.perf_counter()
-    if args.stream:
-        pipe.run_stream(args.steps)
-    else:
-        for _ in range(args.steps):
-            pipe.step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    prof = None
-    if dom is not None:
-        eng.profile(False)
-        prof = eng.profile_read()
+    elapsed, breakdown, prof, dom, stage_timed = timed_run(pipe, eng, args.steps, args.warmup, barrier,
+                                                           profile=not args.no_profile, stream=args.stream)
     rank_info = [[elapsed, W, float(sum(pipe.last.get("all_tokens", pipe.last["tokens"]))), pipe.last["steps"]]]
     if world > 1:
         import torch.distributed as dist
@@ -567,7 +691,6 @@ def main():
         dist.all_gather(parts, te, group=host_group)
         rank_info = [p.tolist() for p in parts]
         elapsed = max(r[0] for r in rank_info)             # the job ends with its slowest rank
-    stage_timed = dict(pipe.stage)
     parity = None
     if rank == 0 and not args.no_parity and sd is not None and args.beam == 1:
         from tests.parity_util import sample_indices
@@ -626,48 +749,7 @@ def main():
         out["config"]["gpus_shared"] = True
         out["config"]["physical_gpus"] = torch.cuda.device_count()
     if prof:
-        kern = {}
-        for k, v in breakdown.items():
-            if v["launches"] == 0:
-                continue
-            kern[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
-                       "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["flops"] else None,
-                       "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["bytes"] else None}
-        out["kernels_one_step"] = kern
-        v = prof[dom]                          # measured over the timed region
-        if dom in ("cross_attn", "self_attn", "select", "dec_other", "logmel") or (v["flops"] == 0):
-            ach = v["bytes"] / (v["ms"] * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4)}
-        else:
-            ach = v["flops"] / (v["ms"] * 1e-3) / 1e12
-            roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
-                    "frac": round(ach / MFMA_BF16_PEAK_TFS, 4)}
-        roof["kernel"] = dom
-        roof["launches"] = v["launches"]
-        roof["avg_launch_us"] = round(1000.0 * v["ms"] / max(v["launches"], 1), 2)
-        roof["traffic"] = None
-        if os.path.isfile(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                roof["traffic"] = tj.get(dom)
-            except Exception:
-                pass
-        if args.beam > 1 and not args.cross_fp8:
-            roof["accounting"] = ("projected cross-attention (beam groups): algorithmic bytes = each active window's "
-                                  "K and V panels (L x 2 x 1500 x d bf16) per launch, counted in-kernel")
-        else:
-            roof["accounting"] = ("factored cross-attention: algorithmic bytes = each active window's encoder output "
-                                  + ("(L x 1500 x d e4m3 + 1500 f32 scales)" if args.cross_fp8 else "(L x 1500 x d bf16)")
-                                  + " + q' per launch, counted in-kernel")
-        out["roofline"] = roof
-        enc_ms = sum(breakdown[k]["ms"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
-        enc_fl = sum(breakdown[k]["flops"] for k in ("enc_gemm", "enc_attn", "crosskv_gemm"))
-        out["encoder_mfma"] = {"achieved_tflops": round(enc_fl / max(enc_ms, 1e-9) / 1e9, 1),
-                               "frac_of_2500": round(enc_fl / max(enc_ms, 1e-9) / 1e9 / MFMA_BF16_PEAK_TFS, 4)}
-        cx = breakdown["cross_attn"]
-        out["decoder_kv_read"] = {"achieved_gbs": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6, 1),
-                                  "frac_of_8000": round(cx["bytes"] / max(cx["ms"], 1e-9) / 1e6 / HBM_PEAK_GBS, 4)}
+        out.update(roofline_block(breakdown, prof, dom, args, beam=args.beam))
     comp = composite_roofline(dims, toks, pipe.last["steps"], len(pipe.prompt), elapsed / args.steps, W)
     out.setdefault("roofline", {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                                 "traffic": None})
@@ -679,6 +761,16 @@ def main():
             out["cpu_baseline"] = cpu_baseline(dims, sd, mean_tok)
         except Exception as e:  # reported, never fatal to the GPU measurement
             out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
+    if run_var:
+        del pipe, eng, pcm_dev, sd
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        vsteps = args.variable_steps or max(2, args.steps // 4)
+        try:
+            out["variable"] = variable_block(args, dims, base_sd, tok, local, vsteps)
+        except Exception as e:  # reported, never fatal to the headline measurement
+            out["variable"] = {"error": str(e)[:300]}
     if json_fd is not None:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

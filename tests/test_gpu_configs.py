@@ -100,6 +100,18 @@ def test_large_v3_greedy_150_windows_vs_oracle(lv3):
     _check_greedy(lv3, "large-v3 greedy 150 windows")
 
 
+def test_large_v3_logmel_vs_oracle(lv3):
+    """The FULL large-v3 engine's features() on the bench's own 150 windows (75 min, 450,001 frames, 128 mel bins,
+    one global clamp) vs oracle/mel.py: the north_star log-mel gate (<= 1e-4) at the headline model."""
+    from oracle import mel as omel
+    x = np.concatenate([speech_like(30.0, i) for i in range(lv3.W)])
+    ref = omel.log_mel(x, lv3.dims.n_mels)
+    got = lv3.mel.cpu().numpy()
+    assert got.shape == ref.shape and got.shape[0] == 128
+    err = float(np.abs(got - ref).max())
+    assert err <= 1e-4, err
+
+
 def test_large_v3_encoder_vs_bf16_oracle(lv3):
     """Encoder output of bench windows vs the oracle's encoder in the engine's numeric format (bf16 rounding at
     the same points as encode_chunk, f32 residual and accumulation)."""

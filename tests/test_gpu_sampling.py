@@ -102,6 +102,48 @@ def test_sampling_matches_oracle_draws(setup, T):
     assert same >= W // 2, same          # a near-tied key or forcing decision diverges the rest of a sample
 
 
+@pytest.mark.parametrize("mfma", [1, 0])
+def test_sampling_projected_rows_end_apart(setup, mfma):
+    """best_of sampling in the PROJECTED cross form (cross_mode 0: what transcribe.py runs for beam / best-of groups)
+    with the MFMA group kernel (cross_mfma 1) and the VALU one (0).  A window's 5 sampled hypotheses end at different
+    steps; every live row must keep its cross-attention after another row of its group has ended (the MFMA kernel
+    once returned for the whole group when its first row was done).  Checked per step: the chosen
+    hypothesis' log-prob records vs the oracle teacher-forced on the same tokens (0.02 nats), and each token within
+    eps of the oracle's best Gumbel key under that hypothesis' noise."""
+    from tests.parity_util import oracle_records, record_deviation
+    dims, eng, orc, encf, W = setup
+    st = dims.specials
+    prompt = [st.sot, st.lang_token("en"), st.transcribe]
+    sup = [st.transcribe, st.translate, st.sot, st.sot_prev, st.sot_lm]
+    nh, seed, T, ML = 5, 23, 0.4, 120
+    eng.set_option("cross_mode", 0)
+    eng.set_option("cross_mfma", mfma)
+    try:
+        eng.reserve(W, W * nh)
+        eng.cross_kv(torch.from_numpy(encf).to(torch.bfloat16).cuda(), 0)
+        res, _ = eng.generate(list(range(W)), [prompt] * W, temperature=T, num_hypotheses=nh, seed=seed,
+                              suppress_tokens=sup, max_length=ML, record_logprobs=True)
+    finally:
+        eng.set_option("cross_mode", 1)
+        eng.set_option("cross_mfma", 1)
+        eng.cross_kv(torch.from_numpy(encf).to(torch.bfloat16).cuda(), 0)
+    lens = [len(r.tokens) for r in res]
+    assert len(set(lens)) > 1, lens
+    opt = GenerateOptions(suppress_tokens=sup, max_length=ML, sampling_temperature=T, num_hypotheses=nh, seed=seed)
+    worst = 0.0
+    for w in range(W):
+        rec = oracle_records(orc, encf[w: w + 1], prompt, [res[w].tokens], 1, st, opt)[0]
+        dev, _ = record_deviation(res[w].token_logprobs, rec)
+        worst = max(worst, float(dev.max()))
+        cross = orc.cross_kv(encf[w: w + 1])
+        ended = len(prompt) + len(res[w].tokens) < ML
+        o = GenerateOptions(suppress_tokens=sup, max_length=ML, sampling_temperature=T, num_hypotheses=nh,
+                            seed=seed, hyp_offset=w * nh)
+        per_j = [_key_margins(orc, cross, prompt, res[w].tokens, st, o, w * nh + j, ended) for j in range(nh)]
+        assert max(m[:, 0].min() for m in per_j) >= -EPS, (w, lens)
+    assert worst <= 0.02, worst
+
+
 class _GpuBackend:
     def __init__(self, m):
         self.m = m

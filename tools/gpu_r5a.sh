@@ -1,0 +1,15 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+# the new projected-form sampling test against the library with the old cross_tf liveness rule (expected to FAIL)
+VLOG_AMD_LIB=$GRAFT_REPO_ROOT/abtmp/libbug.so timeout -k 10 300 python -u -m pytest tests/test_gpu_sampling.py -k projected -v --timeout 200 --timeout-method thread > gpurun_out/t_r5a_bug.log 2>&1
+echo "old-rule library rc=$?"; grep -E "PASSED|FAILED|Error" gpurun_out/t_r5a_bug.log | head
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sampling.py -x -v --timeout 300 --timeout-method thread > gpurun_out/t_r5a.log 2>&1
+rc=$?; tail -15 gpurun_out/t_r5a.log; [ $rc -ne 0 ] && exit $rc
+t0=$(date +%s.%N)
+timeout -k 10 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_r05_a.json 2> gpurun_out/bench_r05_a.err || { tail -30 gpurun_out/bench_r05_a.err; exit 1; }
+t1=$(date +%s.%N)
+echo "wall $(python3 -c "print(round($t1-$t0,1))")"
+python3 -c "
+import json; d=json.load(open('gpurun_out/bench_r05_a.json')); v=d.get('variable',{})
+print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_launch_us'])
+print({k: v.get(k) for k in ('value','ms_per_step','token_length_min_p50_max','decoder_steps','active_row_fraction','error')}, v.get('roofline',{}).get('frac'))"

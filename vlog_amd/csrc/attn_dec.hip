@@ -796,7 +796,13 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
   }
   const int row0 = g * group;
   const int hyp0 = a.row_hyp[row0];
-  if (a.done && a.done[hyp0]) return;
+  // Liveness per ROW: the hypotheses of a sampling group (best_of > 1) end at different steps, so the block runs
+  // while any row of its tile is live and writes only live rows (the VALU group kernel's rule)
+  if (a.done) {
+    const int rr = qt * 128 + tid;
+    const bool live = tid < 128 && rr < group && !a.done[a.row_hyp[row0 + rr]];
+    if (!__syncthreads_or(live)) return;
+  }
   // panels by window slot; without a slot table (the factored form's per-layer projection of the pass's windows)
   // by the pass's window index
   const int slot = a.hyp_slot ? a.hyp_slot[hyp0] : hyp0;
@@ -809,6 +815,7 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
     atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), (unsigned long long)((cap ? 3 : 2) * T * HD * 2));
   const int r = qt * 128 + wv * 32 + ql;
   const bool valid = r < group;
+  const bool live = valid && !(a.done && a.done[a.row_hyp[row0 + r]]);   // output writes only for live rows
   const bool wave_on = qt * 128 + wv * 32 < group;     // wave-uniform: a wave with no row only stages tiles
   const float sl2 = a.scale_log2;
   const int ntt = (T + TF_KT - 1) / TF_KT;
@@ -1070,7 +1077,7 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
     }
     return;
   }
-  if (valid) {
+  if (live) {
     const float inv = cap ? inv_cap : 1.0f / l_run;
     bf16* orow = a.out + (long long)(row0 + r) * a.ldo + h * HD;
 #pragma unroll

@@ -78,8 +78,13 @@ thread_local std::string g_err;
   } while (0)
 
 // Bumped whenever a device buffer moves: a captured step graph holds raw pointers, so a decode loop that
-// captured one re-captures it when this changed (e.g. a refill pass that grew a scratch buffer).
-std::atomic<long long> g_realloc{0};
+// captured one re-captures it when this changed (e.g. a refill pass that grew a scratch buffer).  The counter is
+// PER ENGINE: `guarded` points t_realloc at the engine whose entry point runs on this thread (under its lock), so
+// another engine's allocations neither force a re-capture nor fail a capture in progress.  Allocations outside an
+// entry point (wm_create) count on a fallback no graph reads.
+thread_local long long* t_realloc = nullptr;
+long long g_realloc_none = 0;
+inline long long& realloc_gen() { return t_realloc ? *t_realloc : g_realloc_none; }
 
 struct DevBuf {
   void* p = nullptr;
@@ -91,7 +96,7 @@ struct DevBuf {
     bytes = 0;
     HIP_OK(hipMalloc(&p, b));
     bytes = b;
-    ++g_realloc;
+    ++realloc_gen();
   }
   void release() {
     if (p) (void)hipFree(p);
@@ -131,6 +136,8 @@ struct wm_engine {
   wm_model_dims dm;
   int device;
   std::mutex mu;
+  bool weights_ok = false;     // every weight slot set (cached by require_weights)
+  long long realloc_gen = 0;   // this engine's buffer generation (t_realloc while one of its entry points runs)
   // weights
   std::map<std::string, Slot> slots;
   std::vector<std::string> slot_order;   // weight names in layout order (wm_weight_info)
@@ -913,17 +920,17 @@ void debug_nan(wm_engine* e, float* logits, int rows, hipStream_t s) {
 struct StepGraph {
   hipGraphExec_t exec = nullptr;
   bool capturing = false;
-  long long gen = -1;                       // g_realloc at capture
+  long long gen = -1;                       // realloc_gen() at capture
   void drop() {
     if (exec) (void)hipGraphExecDestroy(exec);
     exec = nullptr;
   }
   // false: buffers moved since the capture (the caller runs an eager step, which re-sizes, then captures again)
-  bool valid() const { return !exec || gen == g_realloc.load(); }
+  bool valid() const { return !exec || gen == realloc_gen(); }
   template <class F> void run(hipStream_t ds, F&& step) {
     if (!exec) {
       hipGraph_t g = nullptr;
-      gen = g_realloc.load();
+      gen = realloc_gen();
       HIP_OK(hipStreamBeginCapture(ds, hipStreamCaptureModeThreadLocal));
       capturing = true;
       step();
@@ -932,7 +939,7 @@ struct StepGraph {
       const hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
       (void)hipGraphDestroy(g);
       HIP_OK(ie);
-      if (gen != g_realloc.load()) throw std::runtime_error("decode step graph: a buffer moved during capture");
+      if (gen != realloc_gen()) throw std::runtime_error("decode step graph: a buffer moved during capture");
     }
     HIP_OK(hipGraphLaunch(exec, ds));
   }
@@ -1872,7 +1879,7 @@ void generate_rows_beam(wm_engine* e, const wm_generate_args* a, hipStream_t st)
         for (int g : set) { n_live += glive[g]; n_free += !glive[g]; }
         if (n_live == 0 && next >= W) break;
         const bool refill = next < W && (n_free >= refill_min || n_live == 0);
-        const bool compact = next >= W && n_live * 8 <= (int)set.size() * 7;
+        const bool compact = a->compact && next >= W && n_live * 8 <= (int)set.size() * 7;   // opt-in, as the header says
         if (refill || compact) {
           nset.clear(); starts.clear();
           for (int g : set) {
@@ -1995,7 +2002,12 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
   // 150-window step, most of it those passes).
   size_t free_b = 0, total_b = 0;
   HIP_OK(hipMemGetInfo(&free_b, &total_b));
-  const double reusable = (double)e->a_attn.bytes + (double)e->a_logits.bytes;
+  // the factored form's alignment pass also gathers each item's encoder output and its per-layer K/V projection
+  // (a_enc + a_kv, 3 x T x d bf16 per item, forward()): counted per item below
+  const bool tf_gather = e->cross_mode == 1 && e->cross_tf && !e->cross_fp8;
+  const double per_item_kv = tf_gather ? 3.0 * (double)T * m.n_state * 2 : 0.0;
+  const double reusable = (double)e->a_attn.bytes + (double)e->a_logits.bytes +
+                          (tf_gather ? (double)e->a_enc.bytes + (double)e->a_kv.bytes : 0.0);
   const double budget = std::max(1.5e9, std::min(48e9, 0.5 * (double)free_b + reusable));
   static const bool align_log = [] {
     const char* v = std::getenv("VLOG_AMD_ALIGN_LOG");
@@ -2014,7 +2026,7 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
     while (i1 < n) {
       const int it = ord[i1];
       const int s2 = std::max(smax, S[it]);
-      const double bytes = (double)(i1 - i0 + 1) * s2 * n_heads * T * 4 + (double)(ntext + nt[it]) * V * 4;
+      const double bytes = (double)(i1 - i0 + 1) * (s2 * n_heads * T * 4 + per_item_kv) + (double)(ntext + nt[it]) * V * 4;
       if (i1 > i0 && (bytes > budget || (double)(i1 - i0 + 1) * s2 > 1.25 * (double)(sum_s + S[it]))) break;
       smax = s2;
       ntext += nt[it];
@@ -2108,6 +2120,11 @@ int guarded(wm_engine* e, F&& f) {
   try {
     if (!e) throw std::runtime_error("null engine");
     std::lock_guard<std::mutex> lk(e->mu);
+    struct GenScope {                     // restored on every exit, exceptions included
+      long long* prev;
+      explicit GenScope(long long* g) : prev(t_realloc) { t_realloc = g; }
+      ~GenScope() { t_realloc = prev; }
+    } gs(&e->realloc_gen);
     HIP_OK(hipSetDevice(e->device));
     f();
     return 0;
@@ -2115,6 +2132,14 @@ int guarded(wm_engine* e, F&& f) {
     g_err = ex.what();
     return -1;
   }
+}
+
+// The model entry points need every weight slot set (an engine made for the front end alone has none)
+void require_weights(wm_engine* e) {
+  if (e->weights_ok) return;
+  for (auto& kv : e->slots)
+    if (!kv.second.set) throw std::runtime_error("engine weights incomplete (front-end-only engine?): " + kv.first);
+  e->weights_ok = true;
 }
 
 }  // namespace
@@ -2282,6 +2307,7 @@ int wm_logmel_finalize(wm_engine* e, float* d_mel, int64_t n_frames, int64_t ld,
 int wm_encode(wm_engine* e, const float* d_mel, int64_t ld, const int32_t* h_seek, const int32_t* h_nframes, int32_t B,
               void* d_enc_out, void* stream) {
   return guarded(e, [&] {
+    require_weights(e);
     check_weights(e);
     hipStream_t st = (hipStream_t)stream;
     const int chunk = std::max(1, e->enc_chunk);
@@ -2306,6 +2332,7 @@ int wm_reserve(wm_engine* e, int32_t n_slots, int32_t n_hyp, void* stream) {
 
 int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void* stream) {
   return guarded(e, [&] {
+    require_weights(e);
     check_weights(e);
     if (slot0 < 0 || slot0 + B > e->n_slots) throw std::runtime_error("wm_cross_kv: slots out of range (wm_reserve first)");
     const auto& m = e->dm;
@@ -2332,12 +2359,16 @@ int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void*
 }
 
 int wm_generate(wm_engine* e, const wm_generate_args* a, void* stream) {
-  return guarded(e, [&] { generate(e, a, (hipStream_t)stream); });
+  return guarded(e, [&] {
+    require_weights(e);
+    generate(e, a, (hipStream_t)stream);
+  });
 }
 
 int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_len, const int32_t* h_tokens, float* d_logits,
                int32_t last_only, const int32_t* h_align_heads, int32_t n_align, float* d_attn, void* stream) {
   return guarded(e, [&] {
+    require_weights(e);
     forward(e, n_seq, h_slots, seq_len, h_tokens, d_logits, last_only, h_align_heads, n_align, d_attn, (hipStream_t)stream);
   });
 }
@@ -2345,6 +2376,7 @@ int wm_forward(wm_engine* e, int32_t n_seq, const int32_t* h_slots, int32_t seq_
 int wm_detect_language(wm_engine* e, int32_t n, const int32_t* h_slots, int32_t lang_begin, int32_t n_langs,
                        float* h_probs, void* stream) {
   return guarded(e, [&] {
+    require_weights(e);
     if (n <= 0) return;
     if (lang_begin < 0 || n_langs <= 0 || lang_begin + n_langs > e->dm.n_vocab)
       throw std::runtime_error("wm_detect_language: language tokens outside the vocabulary");
@@ -2406,6 +2438,7 @@ int wm_align(wm_engine* e, int32_t slot, int32_t sot_len, const int32_t* h_sot, 
              int32_t num_frames, const int32_t* h_heads, int32_t n_heads, int32_t median_filter_width, float* h_probs,
              int32_t* h_text_idx, int32_t* h_time_idx, int32_t* h_path_len, void* stream) {
   return guarded(e, [&] {
+    require_weights(e);
     check_weights(e);
     align(e, slot, sot_len, h_sot, n_text, h_text, num_frames, h_heads, n_heads, median_filter_width, h_probs, h_text_idx,
           h_time_idx, h_path_len, (hipStream_t)stream);
@@ -2417,6 +2450,7 @@ int wm_align_batch(wm_engine* e, int32_t n, const int32_t* h_slots, int32_t sot_
                    int32_t n_heads, int32_t median_filter_width, float* h_probs, const int64_t* h_path_off,
                    int32_t* h_text_idx, int32_t* h_time_idx, int32_t* h_path_len, void* stream) {
   return guarded(e, [&] {
+    require_weights(e);
     check_weights(e);
     for (int i = 0; i < n; ++i)
       if (h_slots[i] < 0 || h_slots[i] >= e->n_slots) throw std::runtime_error("wm_align_batch: slot out of range");

@@ -151,6 +151,9 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
   Cand mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
   Cand gt{-INFINITY, 0x7fffffff}, gs{-INFINITY, 0x7fffffff};
   const int K = MODE == 1 ? p.topk : 0;
+  // Gumbel noise keyed on the WINDOW's hypothesis id, not the slot: the row-set decode reuses slots, and a window's
+  // draws must not depend on which slot it got (hyp_out[h] = w there, one hypothesis per window; h = w*nh + j else)
+  const int gkey = MODE == 2 && p.hyp_out ? p.hyp_out[h] : h;
   // (explicit branches, not a reference chosen per element: a `Cand& m = is_ts ? ms : mt` put both in scratch;
   // a select-only form of this pass spilled)
 #pragma unroll
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(SB) void logits_select_kernel(SearchParams p) {
     if (MODE == 2) {
       // the decode step of this hypothesis = tokens it has sampled so far (equal to the host's step counter
       // for every live hypothesis; read from the device so a captured step graph replays unchanged)
-      const float key = x * p.inv_temperature + gumbel(p.seed, h, len - p.sample_begin, i);
+      const float key = x * p.inv_temperature + gumbel(p.seed, gkey, len - p.sample_begin, i);
       if (is_ts) {
         if (better(key, i, gs.v, gs.i)) { gs.v = key; gs.i = i; }
       } else {

@@ -126,6 +126,27 @@ class GpuEngine:
         if not self.lib.wm_weights_complete(self.h):
             raise RuntimeError("engine weights incomplete")
 
+    @classmethod
+    def frontend(cls, dims: ModelDims, device_index: int = 0) -> "GpuEngine":
+        """An engine handle with NO weights loaded, for the front end alone (log-mel, frame energy, VAD): a shard
+        coordinator needs the features (and the global log-mel max) before any model pass.  wm_create builds the
+        n_mels filterbank, so features() runs the same kernels as a full engine of these dims; the decoder and
+        encoder entry points fail (wm_weights_complete is false)."""
+        self = cls.__new__(cls)
+        self.lib = _capi.load()
+        self.dims = dims
+        self.device = torch.device("cuda", device_index)
+        st = dims.specials
+        cd = _capi.ModelDimsC(dims.n_mels, dims.n_state, dims.n_head, dims.n_enc_layer, dims.n_dec_layer,
+                              dims.n_vocab, dims.n_audio_ctx, dims.n_text_ctx, st.eot, st.sot, st.no_speech,
+                              st.no_timestamps, st.timestamp_begin, st.blank)
+        h = C.c_void_p()
+        _capi.check(self.lib.wm_create(C.byref(cd), device_index, C.byref(h)), "wm_create")
+        self.h = h
+        self.n_slots = 0
+        self.n_hyp = 0
+        return self
+
     def __del__(self):
         h = getattr(self, "h", None)
         if h is not None and h.value:
