@@ -51,14 +51,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_shard(g0: int, W: int, cache=None):
+def build_shard(g0: int, W: int, cache=None, variable: bool = False):
     """PCM of windows [g0, g0 + W) of the corpus plus 200-sample margins from the neighbouring clips (window i is
-    speech_like seed i; `cache` maps seeds already generated to their clips)."""
+    speech_like seed i; variable: the variable corpus, vlog_amd.audio.long_form_window, every 10th window room tone;
+    `cache` maps seeds already generated to their clips)."""
+    from vlog_amd.audio import long_form_window
     cache = {} if cache is None else cache
 
     def clip(i):
         if i not in cache:
-            cache[i] = speech_like(30.0, i)
+            cache[i] = long_form_window(i) if variable else speech_like(30.0, i)
         return cache[i]
     clips = [clip(g0 + i) for i in range(W)]
     left = clip(g0 - 1)[-200:] if g0 > 0 else np.zeros(0, np.float32)
@@ -513,7 +515,7 @@ def variable_block(args, dims, base_sd, tok, local: int, steps: int, warmup: int
     plant_margin(base_sd, dims, 0, variable=True)
     eng = GpuEngine(dims, base_sd, local)
     W = args.windows
-    pcm, margin = build_shard(0, W)
+    pcm, margin = build_shard(0, W, variable=True)
     pcm_dev = torch.from_numpy(pcm).to(eng.device)
     eng.reserve(W, W)
     pipe = Pipeline(eng, tok, dims, 0, 1, W, 1, pcm_dev, margin, W * CLIP, None, check_every=args.check_every,
@@ -569,8 +571,9 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity sample (rank 0, untimed)")
     ap.add_argument("--parity-windows", type=int, default=16)
     ap.add_argument("--workload", choices=("uniform", "variable"), default="uniform",
-                    help="uniform: the margin-planted model (every window ~112 tokens); variable: plant margin_var "
-                         "(a window's audio level sets where its script ends: 1 to ~225 tokens, most 50-150)")
+                    help="uniform: the margin-planted model (every window ~112 tokens); variable: plant margin_var on "
+                         "the variable corpus (a window's audio level sets where its script ends: 44 to ~225 tokens "
+                         "for speech, one token for the room-tone window in every 10)")
     ap.add_argument("--max-rows", type=int, default=None,
                     help="row-set decode with at most this many rows in flight (0 = all windows at once), windows "
                          "ordered longest-expected first, finished rows refilled / compacted; -1 = one all-rows "
@@ -650,7 +653,8 @@ def main():
     W_nat = W = args.windows
     g0 = rank * W
     cache = {}
-    pcm, margin = build_shard(g0, W, cache)
+    var_corpus = args.workload == "variable"
+    pcm, margin = build_shard(g0, W, cache, variable=var_corpus)
     if world > 1 and args.balance == "tokens":
         # work-balanced shards (vlog_amd/shard.py): every rank estimates the expected tokens of its natural window
         # range from the GPU frame energy, the estimates are exchanged as host floats, and the corpus is re-cut into
@@ -663,7 +667,7 @@ def main():
         dist.all_gather(parts, est, group=host_group)
         g0, g1 = partition_by_weight(torch.cat(parts).numpy(), world)[rank]
         W = g1 - g0
-        pcm, margin = build_shard(g0, W, cache)
+        pcm, margin = build_shard(g0, W, cache, variable=var_corpus)
     del cache
     pcm_dev = torch.from_numpy(pcm).to(eng.device)
     n_total = world * W_nat * CLIP

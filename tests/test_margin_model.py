@@ -77,9 +77,12 @@ def tiny_var():
     w = round_bf16(sd)
     o32 = OracleWhisper(w, dims, np.float32)
     o16 = OracleWhisper(w, dims, np.float32, bf16_acts=True)
-    # windows of the corpus with levels from 8 to -4 (measured): one token to ~150
+    # windows of the corpus with levels from 8 to -4 (measured): five tokens to ~150; plus window 9 of the
+    # variable corpus (room tone: the quiet bit ends it after one token)
+    from vlog_amd.audio import long_form_window
     seeds = [10, 0, 3, 4, 12, 1, 2]
-    x = np.concatenate([speech_like(30.0, s) for s in seeds])
+    x = np.concatenate([speech_like(30.0, s) for s in seeds] + [long_form_window(9)])
+    seeds = seeds + [9]
     n = len(seeds)
     mel = omel.log_mel(x, dims.n_mels)[:, :3000 * n].reshape(dims.n_mels, n, 3000).transpose(1, 0, 2)
     enc = o32.encode(np.ascontiguousarray(mel))
@@ -93,15 +96,20 @@ def tiny_var():
 def test_variable_length_follows_the_window_level(tiny_var):
     """The script ends after the first exit timestamp whose threshold the window's level exceeds: lengths from
     1 token to the whole script, each an exact prefix of the planted script (+ its timestamp pairs)."""
-    from vlog_amd.weights import level_weights
+    from vlog_amd.weights import QUIET_W, level_weights
     dims, plan, _, enc, _, _, _, res = tiny_var
     LEVEL_W = level_weights(dims.n_mels)
     c, cr = plan.bit_channels
     lengths = []
+    quiet = []
     for i, r in enumerate(res):
-        s = np.sign((enc[i][:, c] - enc[i][:, cr]).mean(0))[:6]
+        bits = np.sign((enc[i][:, c] - enc[i][:, cr]).mean(0))
+        s = bits[:6]
+        q = int(bits[7]) * plan.quiet_sign                 # +1: the window is silence
+        quiet.append(q)
         L = int(sum(w * b for w, b in zip(LEVEL_W, s)))
-        k_exit = next((k for k, T in plan.exits if L > T), len(plan.slots) - 1)
+        k_exit = next((k for e, (k, T) in enumerate(plan.exits) if L + (QUIET_W * q if e == 0 else 0) > T),
+                      len(plan.slots) - 1)
         flat, k, pos = list(r.tokens), 0, 0
         while True:                                   # walk the script up to the exit slot
             slot, kind = plan.slots[k], plan.kinds[k]
@@ -116,8 +124,11 @@ def test_variable_length_follows_the_window_level(tiny_var):
         assert pos == len(flat), (i, L, pos, len(flat))
         assert r.score > -1e-3
         lengths.append((L, len(flat)))
-    # a higher level ends earlier; the levels of these windows span one token to ~150+
-    by_level = sorted(lengths, key=lambda t: -t[0])
+    # the room-tone window is the only quiet one and decodes one token (its first timestamp)
+    assert quiet == [-1] * (len(res) - 1) + [1], quiet
+    assert lengths[-1][1] == 1, lengths
+    # among the speech windows a higher level ends earlier; their levels span five tokens to ~150+
+    by_level = sorted(lengths[:-1], key=lambda t: -t[0])
     assert all(a[1] < b[1] for a, b in zip(by_level, by_level[1:]) if a[0] > b[0]), lengths
     assert by_level[0][1] <= 5 and by_level[-1][1] >= 140, lengths
 

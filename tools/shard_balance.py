@@ -33,7 +33,7 @@ def main():
     cache = {}
     est = []
     for r in range(world):                                # each rank's estimate of its natural range
-        pcm, margin = bench.build_shard(r * Wn, Wn, cache)
+        pcm, margin = bench.build_shard(r * Wn, Wn, cache, variable=True)
         db = eng.frame_energy_db(torch.from_numpy(pcm), 512)
         est.append(expected_tokens(db, 512, [margin + bench.CLIP * i for i in range(Wn)], [bench.CLIP] * Wn))
     est = np.concatenate(est)
@@ -44,7 +44,7 @@ def main():
         ranks = []
         for r, (g0, g1) in enumerate(parts):
             W = g1 - g0
-            pcm, margin = bench.build_shard(g0, W, cache)
+            pcm, margin = bench.build_shard(g0, W, cache, variable=True)
             pipe = bench.Pipeline(eng, tok, dims, 0, 1, W, 1, torch.from_numpy(pcm).to(eng.device), margin, n_total,
                                   g0=g0, max_rows=0)
             pipe.step()                                   # warm-up (graphs, buffers)

@@ -111,6 +111,29 @@ def speech_like(seconds: float, seed: int = 0, sr: int = SR, as_int16: bool = Fa
     return x16 if as_int16 else x16.astype(np.float32) / 32768.0
 
 
+def room_tone(seconds: float, seed: int = 0, sr: int = SR, dbfs: float = -70.0, as_int16: bool = False) -> np.ndarray:
+    """Silence as a recording has it: low-level pink-ish room noise at `dbfs` RMS (int16-quantised like
+    speech_like), e.g. the gaps between the parts of a long-form programme."""
+    rng = np.random.default_rng(10_000_019 + seed)
+    n = int(round(seconds * sr))
+    x = lfilter([1.0], [1.0, -0.9], rng.standard_normal(n))
+    x *= (10 ** (dbfs / 20)) / (np.sqrt(np.mean(x ** 2)) + 1e-12)
+    x16 = np.clip(np.round(x * 32768.0), -32768, 32767).astype(np.int16)
+    return x16 if as_int16 else x16.astype(np.float32) / 32768.0
+
+
+QUIET_EVERY = 10
+
+
+def long_form_window(i: int, seconds: float = 30.0) -> np.ndarray:
+    """Window i of the variable-length corpus (bench.py --workload variable, the variable gates): speech_like(seed i),
+    except every QUIET_EVERY-th window (i % QUIET_EVERY == QUIET_EVERY - 1) is room tone, so the corpus holds the
+    near-empty windows (silence between programme parts) real long-form audio has."""
+    if i % QUIET_EVERY == QUIET_EVERY - 1:
+        return room_tone(seconds, i)
+    return speech_like(seconds, i)
+
+
 def corpus(n_clips: int, clip_seconds: float = 30.0, seed0: int = 0) -> np.ndarray:
     """Concatenation of n_clips speech-like clips with seeds seed0 .. seed0+n_clips-1 (float32)."""
     return np.concatenate([speech_like(clip_seconds, seed0 + i) for i in range(n_clips)])

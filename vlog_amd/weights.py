@@ -174,6 +174,8 @@ class MarginPlan:
     # variable-length script (plant "margin_var"): (slot k of a timestamp, threshold T) — the window ends with
     # <|endoftext|> right after that timestamp when its level L = sum_j LEVEL_W[j] * bit_j exceeds T (first such k)
     exits: List[Tuple[int, int]] = field(default_factory=list)
+    # variable plant: the sign the quiet bit carries for a silent window (bit_channels[.][7])
+    quiet_sign: int = 0
 
 
 # Variable-length script (plant "margin_var"): 16 segments (up to ~225 tokens), level weights of the six bits (bit 0,
@@ -185,6 +187,9 @@ class MarginPlan:
 #   -6 -> ~179, -8 -> the whole script (~222); mean ~97 over the level distribution.
 VAR_SEGMENTS = 16
 LEVEL_W = (-3, 1, 1, 1, 1, 1)
+# the quiet bit's weight in the first exit's test (a silent window's level clears T = 7 whatever its other bits; a
+# speech window's never does)
+QUIET_W = 16
 
 
 def level_weights(n_mels: int) -> Tuple[int, ...]:
@@ -285,9 +290,14 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
     ch = rng.choice(d, size=6 * nb, replace=False)
     s_ch, s_ref, m_ch, m_ref, c_ch, c_ref = (ch[i * nb:(i + 1) * nb] for i in range(6))
     k_ch = k_ref = None
+    qch = None
     if variable:
         rng_v = np.random.default_rng(int.from_bytes(hashlib.sha256(f"{seed}:plant_margin_var".encode()).digest()[:8], "little"))
         k_ch, k_ref = (int(c) for c in rng_v.choice(np.setdiff1d(np.arange(d), ch), size=2, replace=False))
+        # the quiet bit's six channels (stem, its reference, window mean, its reference, carrier, its reference),
+        # drawn after the constant bit's two
+        qch = [int(c) for c in rng_v.choice(np.setdiff1d(np.arange(d), np.concatenate([ch, [k_ch, k_ref]])), size=6,
+                                            replace=False)]
     cal = _margin_calib(dims.n_mels)
     P = torch.tensor(cal["proj"], dtype=torch.float32)               # [n_mels, nb]
     med, fstd = cal["median"], cal["frame_std"]
@@ -297,9 +307,20 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
     c1w, c1b = sd["model.encoder.conv1.weight"], sd["model.encoder.conv1.bias"]       # [d, n_mels, 3]
     c2w, c2b = sd["model.encoder.conv2.weight"], sd["model.encoder.conv2.bias"]       # [d, d, 3]
     gelu_b1 = float(0.5 * b1 * (1.0 + math.erf(b1 / math.sqrt(2.0))))
-    if variable:                                         # the constant bit's channels: no stem writes either
-        for c in (k_ch, k_ref):
+    if variable:                                         # the constant and quiet bits' channels: no stem writes
+        for c in [k_ch, k_ref] + qch:
             c1w[c] = 0.0; c1b[c] = 0.0; c2w[c] = 0.0; c2b[c] = 0.0
+        # quiet bit: bit 0's projection centred at the calibrated quiet threshold (between speech and room tone)
+        # instead of the corpus median, so its sign says "this window is silence"
+        qs, qs_ref = qch[0], qch[1]
+        thr_q = float(cal["quiet"]["threshold"])
+        c1w[qs, :, 1] = g1[0] * P[:, 0]
+        c1b[qs] = b1 - g1[0] * thr_q
+        c1b[qs_ref] = b1
+        c2w[qs, qs, 1] = 1.0
+        c2w[qs_ref, qs_ref, 1] = 1.0
+        c2b[qs] = b1 - gelu_b1
+        c2b[qs_ref] = b1 - gelu_b1
     for j in range(nb):
         for c in (s_ch[j], s_ref[j], m_ch[j], m_ref[j], c_ch[j], c_ref[j]):
             c1w[c] = 0.0; c1b[c] = 0.0; c2w[c] = 0.0; c2b[c] = 0.0
@@ -313,7 +334,7 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
     pos = sd["model.encoder.embed_positions.weight"]
     pos[:, torch.as_tensor(ch)] = 0.0
     if variable:
-        pos[:, [k_ch, k_ref]] = 0.0
+        pos[:, [k_ch, k_ref] + qch] = 0.0
     # layer 0, head h_e: uniform attention (q = 0) averaging (LN[s] - LN[s']) into channel m
     h_e = 0
     p0 = "model.encoder.layers.0.self_attn."
@@ -327,11 +348,17 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
     for j in range(nb):
         sd[p0 + "v_proj.weight"][h_e * hd + j, s_ch[j]] = 1.0
         sd[p0 + "v_proj.weight"][h_e * hd + j, s_ref[j]] = -1.0
+    if variable:                                         # the quiet bit's window mean: head dimension nb
+        sd[p0 + "v_proj.weight"][h_e * hd + nb, qch[0]] = 1.0
+        sd[p0 + "v_proj.weight"][h_e * hd + nb, qch[1]] = -1.0
     # the layer-0 LayerNorm affines of s and s' equal, so LN[s] - LN[s'] is the stem difference / sigma_t alone
     ln0w, ln0b = sd["model.encoder.layers.0.self_attn_layer_norm.weight"], sd["model.encoder.layers.0.self_attn_layer_norm.bias"]
     ln0w[torch.as_tensor(s_ref)] = ln0w[torch.as_tensor(s_ch)]
     ln0b[torch.as_tensor(s_ref)] = ln0b[torch.as_tensor(s_ch)]
-    prot = torch.as_tensor(np.concatenate([m_ch, m_ref, c_ch, c_ref] + ([[k_ch, k_ref]] if variable else [])))
+    if variable:
+        ln0w[qch[1]] = ln0w[qch[0]]
+        ln0b[qch[1]] = ln0b[qch[0]]
+    prot = torch.as_tensor(np.concatenate([m_ch, m_ref, c_ch, c_ref] + ([[k_ch, k_ref], qch[2:]] if variable else [])))
     for i in range(dims.n_enc_layer):
         p = f"model.encoder.layers.{i}."
         for w in ("self_attn.out_proj", "fc2"):
@@ -340,6 +367,8 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
     for j in range(nb):
         # window-mean of (LN[s] - LN[s']) has spread ~ spread_j / 0.72 (layer-0 LN std: the sinusoid table)
         sd[p0 + "out_proj.weight"][m_ch[j], h_e * hd + j] = float(s_enc * 0.72 / spread[j])
+    if variable:
+        sd[p0 + "out_proj.weight"][qch[2], h_e * hd + nb] = float(s_enc * 0.72 / spread[0])
 
     def same_affine(ln: str, a, b):
         w_, b_ = sd[ln + ".weight"], sd[ln + ".bias"]
@@ -350,6 +379,8 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
     # o/2s * (GELU(s(Ky + 1)) - GELU(s(Ky - 1))) - o/2 = clip(Ky, -1, 1) * o/2 with the zero exactly at y = 0,
     # since GELU(x) - GELU(-x) = x), so all but a sliver of windows carry a full-size bit
     same_affine("model.encoder.layers.0.final_layer_norm", m_ch, m_ref)
+    if variable:
+        same_affine("model.encoder.layers.0.final_layer_norm", [qch[2]], [qch[3]])
     pf = "model.encoder.layers.0."
     f1w, f1b, f2w, f2b = (sd[pf + n] for n in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
     # the variable-length plant reads the bits' signs as a level too: a 20x steeper clip leaves a 20x thinner sliver
@@ -377,20 +408,32 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
         f2w[k_ch, 2 * nb] = o_half / s_g
         f2w[k_ch, 2 * nb + 1] = -o_half / s_g
         f2b[k_ch] = -o_half
+        # the quiet bit: the same saturating clip of its window mean into its carrier
+        qm, qm_ref, qc, qc_ref = qch[2:]
+        for u, sgn in ((2 * nb + 2, 1.0), (2 * nb + 3, -1.0)):
+            f1w[u] = 0.0
+            f1w[u, qm] = s_g * K
+            f1w[u, qm_ref] = -s_g * K
+            f1b[u] = sgn * s_g
+            f2w[:, u] = 0.0
+        f2w[qc, 2 * nb + 2] = o_half / s_g
+        f2w[qc, 2 * nb + 3] = -o_half / s_g
+        f2b[qc] = -o_half
         lnw, lnb = sd["model.encoder.layer_norm.weight"], sd["model.encoder.layer_norm.bias"]
-        carry = torch.as_tensor(np.concatenate([c_ch, c_ref, [k_ch, k_ref]]))
+        carry = torch.as_tensor(np.concatenate([c_ch, c_ref, [k_ch, k_ref, qc, qc_ref]]))
         lnw[carry] = 1.0
         lnb[carry] = 0.0
 
     # ---- decoder: orthonormal directions
     slot_dirs = len(plan.slots)
-    n_dirs = slot_dirs + nb + 4 + (1 if variable else 0)
+    n_dirs = slot_dirs + nb + 4 + (2 if variable else 0)
     q, _ = torch.linalg.qr(torch.randn(d, n_dirs, generator=g, dtype=torch.float64))
     V = q.T.float()                                      # rows: unit, mutually orthogonal
     v_slot = V[:slot_dirs]
     v_bit = V[slot_dirs: slot_dirs + nb]
     v_sot, v_en, v_eot, v_task = V[slot_dirs + nb: slot_dirs + nb + 4]
     v_const = V[slot_dirs + nb + 4] if variable else None
+    v_quiet = V[slot_dirs + nb + 5] if variable else None
     N = _resid_std(dims.n_dec_layer) * math.sqrt(d)     # norm of the random residual at the final LayerNorm
     R = 6.0 * N                                         # planted token embedding norm
     Bn = 5.0 * R                                        # successor write (> alpha * the largest bit term)
@@ -427,6 +470,9 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
         sd[pc + "v_proj.weight"][h_d * hd + nb, k_ch] = 1.0
         sd[pc + "v_proj.weight"][h_d * hd + nb, k_ref] = -1.0
         sd[pc + "out_proj.weight"][:, h_d * hd + nb] = S_d * v_const
+        sd[pc + "v_proj.weight"][h_d * hd + nb + 1, qch[4]] = 1.0
+        sd[pc + "v_proj.weight"][h_d * hd + nb + 1, qch[5]] = -1.0
+        sd[pc + "out_proj.weight"][:, h_d * hd + nb + 1] = S_d * v_quiet
     # layer-0 MLP successor table
     pm = "model.decoder.layers.0."
     fc1w, fc1b = sd[pm + "fc1.weight"], sd[pm + "fc1.bias"]
@@ -476,9 +522,12 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
             sd[pl + "final_layer_norm.bias"][:] = 0.0
         f1a, b1a, f2a, b2a = (sd[p2 + n] for n in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
         s_c, K_c = 8.0, 5.0 * scale
+        # the first exit (one token: the window ends after its first timestamp) tests L + QUIET_W q_s - T, q_s = +1 for
+        # a silent window: every silent window ends there, no speech window does (|L| <= 8)
+        q_sign = 1.0 if float(cal["quiet"]["silence"]) > thr_q else -1.0
         for e, (k, T) in enumerate(plan.exits):
             for u, sgn in ((2 * e, 1.0), (2 * e + 1, -1.0)):
-                f1a[u] = s_c * K_c * (lev - T * v_const)
+                f1a[u] = s_c * K_c * (lev - T * v_const + (QUIET_W * q_sign * v_quiet if e == 0 else 0.0))
                 b1a[u] = sgn * s_c
                 f2a[:, u] = sgn * (o_I / s_c) * v_ind[e]
             b2a -= o_I * v_ind[e]
@@ -498,8 +547,10 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
             f2b3[:, ua] = Bx * v_eot
             f2b3[:, ub] = -Bx * v_eot
         b2b3 -= M * v_ball
-    plan.bit_channels = ([int(c) for c in c_ch] + ([k_ch] if variable else []),
-                         [int(c) for c in c_ref] + ([k_ref] if variable else []))
+    plan.bit_channels = ([int(c) for c in c_ch] + ([k_ch, qch[4]] if variable else []),
+                         [int(c) for c in c_ref] + ([k_ref, qch[5]] if variable else []))
+    if variable:
+        plan.quiet_sign = 1 if float(cal["quiet"]["silence"]) > float(cal["quiet"]["threshold"]) else -1
     return plan
 
 
