@@ -108,7 +108,7 @@ def test_variable_length_follows_the_window_level(tiny_var):
         q = int(bits[7]) * plan.quiet_sign                 # +1: the window is silence
         quiet.append(q)
         L = int(sum(w * b for w, b in zip(LEVEL_W, s)))
-        k_exit = next((k for e, (k, T) in enumerate(plan.exits) if L + (QUIET_W * q if e == 0 else 0) > T),
+        k_exit = next((k for e, (k, T) in enumerate(plan.exits) if (QUIET_W * q if e == 0 else L) > T),
                       len(plan.slots) - 1)
         flat, k, pos = list(r.tokens), 0, 0
         while True:                                   # walk the script up to the exit slot

@@ -187,9 +187,10 @@ class MarginPlan:
 #   -6 -> ~179, -8 -> the whole script (~222); mean ~97 over the level distribution.
 VAR_SEGMENTS = 16
 LEVEL_W = (-3, 1, 1, 1, 1, 1)
-# the quiet bit's weight in the first exit's test (a silent window's level clears T = 7 whatever its other bits; a
-# speech window's never does)
-QUIET_W = 16
+# the quiet bit's weight in the first exit's test (QUIET_W - 7 > 0 for a silent window, -QUIET_W - 7 < 0 for speech)
+# and the slope of its encoder clip
+QUIET_W = 14
+K_Q = 2.0
 
 
 def level_weights(n_mels: int) -> Tuple[int, ...]:
@@ -408,12 +409,16 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
         f2w[k_ch, 2 * nb] = o_half / s_g
         f2w[k_ch, 2 * nb + 1] = -o_half / s_g
         f2b[k_ch] = -o_half
-        # the quiet bit: the same saturating clip of its window mean into its carrier
+        # the quiet bit: the saturating clip of its window mean into its carrier, with a gentle slope K_Q: every
+        # window sits >= 2.5 spreads from the quiet threshold, so it saturates all the same, and its GELU units stay
+        # below 256 where bf16 resolves their difference (the data bits' K = 1000 units reach ~1e5, where bf16 keeps
+        # nothing of the 2 s_g difference: deterministic, but not the designed magnitude, on a window whose positions
+        # are all alike, as room tone's are)
         qm, qm_ref, qc, qc_ref = qch[2:]
         for u, sgn in ((2 * nb + 2, 1.0), (2 * nb + 3, -1.0)):
             f1w[u] = 0.0
-            f1w[u, qm] = s_g * K
-            f1w[u, qm_ref] = -s_g * K
+            f1w[u, qm] = s_g * K_Q
+            f1w[u, qm_ref] = -s_g * K_Q
             f1b[u] = sgn * s_g
             f2w[:, u] = 0.0
         f2w[qc, 2 * nb + 2] = o_half / s_g
@@ -522,12 +527,13 @@ def plant_margin(sd: Dict[str, torch.Tensor], dims: ModelDims, seed: int = 0, va
             sd[pl + "final_layer_norm.bias"][:] = 0.0
         f1a, b1a, f2a, b2a = (sd[p2 + n] for n in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
         s_c, K_c = 8.0, 5.0 * scale
-        # the first exit (one token: the window ends after its first timestamp) tests L + QUIET_W q_s - T, q_s = +1 for
-        # a silent window: every silent window ends there, no speech window does (|L| <= 8)
+        # the first exit (one token: the window ends after its first timestamp) reads the quiet bit alone:
+        # QUIET_W q_s - T, q_s = +1 for a silent window, so every silent window ends there and no speech window does
         q_sign = 1.0 if float(cal["quiet"]["silence"]) > thr_q else -1.0
         for e, (k, T) in enumerate(plan.exits):
+            test = QUIET_W * q_sign * v_quiet - T * v_const if e == 0 else lev - T * v_const
             for u, sgn in ((2 * e, 1.0), (2 * e + 1, -1.0)):
-                f1a[u] = s_c * K_c * (lev - T * v_const + (QUIET_W * q_sign * v_quiet if e == 0 else 0.0))
+                f1a[u] = s_c * K_c * test
                 b1a[u] = sgn * s_c
                 f2a[:, u] = sgn * (o_I / s_c) * v_ind[e]
             b2a -= o_I * v_ind[e]
