@@ -22,7 +22,7 @@ int main(int argc, char** argv) {
   bf16 *enc, *qp, *pu;
   float *pml, *scale;
   int *slot, *rh;
-  CK(hipMalloc(&enc, (size_t)W * T * d * 2));
+  CK(hipMalloc(&enc, (size_t)W * ((T + 31) / 32) * 32 * d * 2));   // tile-blocked slots (T padded)
   CK(hipMalloc(&qp, (size_t)W * H * d * 2));
   CK(hipMalloc(&pu, (size_t)16 * W * H * d * 2));
   CK(hipMalloc(&pml, (size_t)16 * W * H * 2 * 4));
@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(slot, id.data(), W * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(rh, id.data(), W * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(scale, one.data(), one.size() * 4, hipMemcpyHostToDevice));
-  CK(hipMemset(enc, 0x3c, (size_t)W * T * d * 2));   // bf16 ~0.0117 / e4m3 0x3c = 1.5: finite scores
+  CK(hipMemset(enc, 0x3c, (size_t)W * ((T + 31) / 32) * 32 * d * 2));   // bf16 ~0.0117 / e4m3 0x3c = 1.5: finite scores
   CK(hipMemset(qp, 0x3c, (size_t)W * H * d * 2));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));

@@ -244,12 +244,14 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   constexpr int EB = F8 ? 1 : 2;                         // bytes per stored E element
   const char* E = (const char*)a.enc + ((long long)slot * a.T * a.d + cb) * EB;
   const float* Es = F8 ? a.escale + (long long)slot * a.T : nullptr;
-  // DEPTH 3 (split staging): per wave, rows 0-15 of a tile land by LDS-DMA in one of two 16-row images (one tile
-  // ahead) and rows 16-31 come through registers two tiles ahead into a third 16-row image: 15 KB of E in flight per
-  // wave instead of 10 KB, at the same 40 staging VGPRs.  Otherwise one 32-row image per wave.
-  constexpr int IMGR = DEPTH == 3 ? 48 : 32;              // image rows per wave
+  // bf16: the slot is stored tile-blocked (xblock_kernel): [tile][wave][32 rows][QW], so one wave's 32 x QW slice of a
+  // tile is ONE contiguous, 128-B-aligned 10 KB run and every load is whole cache lines (row-major, each 320-B wave
+  // row slice straddled three 128-B lines: 1.2-1.3x the line requests).  F8 keeps the row-major e4m3 image.
+  const int n_tiles = (a.T + 31) / 32;
+  const char* EB16 = (const char*)a.enc + ((long long)slot * n_tiles * NW + wv) * (32LL * QW * 2);
+  constexpr int IMGR = 32;                                // image rows per wave
   bf16* sE = (bf16*)smem + wv * IMGR * LDR;
-  bf16* sER = DEPTH == 3 ? sE + 32 * LDR : sE + 16 * LDR; // rows 16-31 (DEPTH 3: the register-fed image)
+  bf16* sER = sE + 16 * LDR;                              // rows 16-31
   float* sX = (float*)(smem + NW * IMGR * LDR * 2);      // [NW][16][64] S^T partials
   float* sRed = sX + NW * 16 * 64;                       // [16][64] their sums
   {
@@ -275,8 +277,8 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
 
   // Address arithmetic is recomputed from an opaque copy of the lane id inside the loop (`lo`), so the
   // compiler does not hoist ~40 loop-invariant addresses into registers the accumulators need.
-  i32x4 stgA[LS], stgB[LS];
-  float scA = 1.f, scB = 1.f;            // F8: lane l (< 32) stages the scale of position tile*32 + l
+  i32x4 stgA[LS];
+  float scA = 1.f;                       // F8: lane l (< 32) stages the scale of position tile*32 + l
   auto load = [&](i32x4 (&stg)[LS], float& scl, int tile, int lo) {
     if (ABL & 16) {                    // ablation: no E loads (compute-only timing)
 #pragma unroll
@@ -286,9 +288,16 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     }
 #pragma unroll
     for (int i = 0; i < LS; ++i) {
-      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
-      const int t = min(tile * 32 + r, a.T - 1);
-      const i32x4* src = (const i32x4*)(E + ((long long)t * a.d) * EB + ch * 16);
+      const int idx = i * 64 + lo;
+      const i32x4* src;
+      if constexpr (F8) {
+        const int r = idx / CPR, ch = idx - r * CPR;
+        const int t = min(tile * 32 + r, a.T - 1);
+        src = (const i32x4*)(E + ((long long)t * a.d) * EB + ch * 16);
+      } else {
+        // chunk idx = (r, ch) of the wave's slice, stored at byte 16 idx of its tile block (rows past T are zeros)
+        src = (const i32x4*)(EB16 + (long long)tile * NW * (32LL * QW * 2) + idx * 16);
+      }
       if (ABL & 8) stg[i] = *src;
       else stg[i] = __builtin_nontemporal_load(src);
     }
@@ -296,55 +305,17 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   };
   float* sScale = nullptr;
   if (F8) sScale = (float*)(smem + NW * IMGR * LDR * 2 + (NW + 1) * 16 * 64 * 4) + wv * 32;
-  // DEPTH 3 loads.  Rows 16-31 of a tile: LS / 2 16-B loads per lane into a register half-set; rows 0-15: LS / 2
-  // LDS-DMA wave-instructions of 1 KiB each, lane-linear in the 16-row image, so each lane fetches the chunk that
-  // the image's swizzle puts at its destination slot (c = slot ^ ((row >> 2) & 3), the inverse of xchunk).
-  constexpr int LH = LS / 2;
-  auto load_hi = [&](i32x4 (&stg)[LH], int tile, int lo) {
-#pragma unroll
-    for (int i = 0; i < LH; ++i) {
-      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
-      const int t = min(tile * 32 + 16 + r, a.T - 1);
-      stg[i] = __builtin_nontemporal_load((const i32x4*)(E + ((long long)t * a.d) * EB + ch * 16));
-    }
-  };
-  auto store_hi = [&](const i32x4 (&stg)[LH], int lo) {
-#pragma unroll
-    for (int i = 0; i < LH; ++i) {
-      const int idx = i * 64 + lo, r = idx / CPR, ch = idx - r * CPR;
-      *(i32x4*)(sER + r * LDR + 8 * xchunk(r, ch)) = stg[i];
-    }
-  };
-  auto dma_lo = [&](int tile, int buf, int lo) {
-    bf16* img = sE + buf * 16 * LDR;
-#pragma unroll
-    for (int i = 0; i < LH; ++i) {
-      const int pb = i * 1024 + 16 * lo;                 // byte offset of this lane's 16 B in the image
-      const int r = pb / (LDR * 2), sl = (pb - r * LDR * 2) >> 4;
-      const int c = sl ^ ((r >> 2) & 3);
-      const int t = min(tile * 32 + r, a.T - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(E + ((long long)t * a.d) * EB + c * 16),
-                                       (__attribute__((address_space(3))) void*)(img + i * 512), 16, 0, 2);
-    }
-  };
   float* pr_row = nullptr;
   if (a.probs && wv == 0 && valid) {
     const int hm = a.head_map[hd];
     if (hm >= 0) pr_row = a.probs + ((long long)row * a.n_align + hm) * a.T;
   }
-  // one tile: its staged registers -> the wave's LDS image, the loads of tile + DEPTH into the same
+  // one tile: its staged registers -> the wave's LDS image, the loads of the next tile into the same
   // registers, then S^T, the cross-wave sum, the online softmax and U^T
-  auto tile_step = [&](int tile, auto& stg, float& scl, int buf) {
+  auto tile_step = [&](int tile, auto& stg, float& scl) {
     int lo = lane;
     asm volatile("" : "+v"(lo));
-    bf16* sEA = DEPTH == 3 ? sE + buf * 16 * LDR : sE;    // rows 0-15 of this tile
-    if constexpr (DEPTH == 3) {
-      // this tile's rows 16-31 (registers) to their image, then the loads two tiles ahead into the same registers
-      // and the DMA of the next tile's rows 0-15; rows 0-15 of THIS tile were retired by the caller's vmcnt
-      store_hi(stg, lo);
-      if (tile + 1 < te) dma_lo(tile + 1, buf ^ 1, lo);
-      if (tile + 2 < te) load_hi(stg, tile + 2, lo);
-    } else {
+    bf16* sEA = sE;                                       // rows 0-15 of this tile
     // wave-private LDS image of this tile (this wave's earlier reads of it are complete: LDS is in order);
     // F8: each 16-B chunk of 16 e4m3 values becomes two bf16 chunks (exact: e4m3 is a subset of bf16)
     int r = lo / CPR, ch = lo % CPR;     // chunk (r, ch) of load i, stepped like the global offsets
@@ -374,8 +345,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
       }
     }
     if (F8 && lo < 32) sScale[lo] = scl;
-    if (tile + DEPTH < te) load(stg, scl, tile + DEPTH, lo);
-    }
+    if (tile + 1 < te) load(stg, scl, tile + 1, lo);
     // ---- S^T partial over this wave's columns
     f32x16 sc = xzero16();
     {
@@ -397,7 +367,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
     if (!(ABL & 2)) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sX[(wv * 16 + r) * 64 + lane] = sc[r];
-      xbarrier<DEPTH == 3>();
+      xbarrier<false>();
       // wave w sums registers r = w, w + NW, ... over the waves in order 0..NW-1 (any NW)
 #pragma unroll
       for (int k = 0; k < (16 + NW - 1) / NW; ++k) {
@@ -408,7 +378,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
         for (int w2 = 1; w2 < NW; ++w2) v += sX[(w2 * 16 + r) * 64 + lane];
         sRed[r * 64 + lane] = v;
       }
-      xbarrier<DEPTH == 3>();
+      xbarrier<false>();
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc[r] = sRed[r * 64 + lane];
     }
@@ -467,33 +437,6 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
       const int lowc = 2 * (G4 & 1) + (gp >> 1);
       const int o0 = (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
       const int o1 = (8 + 4 * hh + gq) * LDR + 8 * (lowc ^ (2 + hh)) + 4 * (gp & 1);
-      if constexpr (DEPTH == 3) {
-        // transposed reads as inline asm: the compiler gives the tr16 intrinsic no alias information and would
-        // drain vmcnt (the next tiles' DMA and loads) before it; this tile's images were retired by the tile's
-        // vmcnt, and the DMA in flight writes the other buffer.  Each c's four reads, then their lgkmcnt.
-        auto lds_addr = [](const bf16* p) -> unsigned {
-          return (unsigned)(size_t)(__attribute__((address_space(3))) const bf16*)p;
-        };
-        const unsigned a00 = lds_addr(sEA + o0), a01 = lds_addr(sEA + o1);
-        const unsigned a10 = lds_addr(sER + o0), a11 = lds_addr(sER + o1);
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          xi32x2 r00, r01, r10, r11;
-          asm volatile(
-              "ds_read_b64_tr_b16 %0, %4 offset:%8\n\t"
-              "ds_read_b64_tr_b16 %1, %5 offset:%8\n\t"
-              "ds_read_b64_tr_b16 %2, %6 offset:%8\n\t"
-              "ds_read_b64_tr_b16 %3, %7 offset:%8\n\t"
-              "s_waitcnt lgkmcnt(0)"
-              : "=v"(r00), "=v"(r01), "=v"(r10), "=v"(r11)
-              : "v"(a00), "v"(a01), "v"(a10), "v"(a11), "i"(64 * c)
-              : "memory");
-          const bf16x8 va0 = __builtin_bit_cast(bf16x8, i32x4{r00[0], r00[1], r01[0], r01[1]});
-          const bf16x8 va1 = __builtin_bit_cast(bf16x8, i32x4{r10[0], r10[1], r11[0], r11[1]});
-          o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, pf[0], o[c], 0, 0, 0);
-          o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, pf[1], o[c], 0, 0, 0);
-        }
-      } else
 #pragma unroll
       for (int c = 0; c < CT; ++c)
 #pragma unroll
@@ -511,33 +454,8 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
         }
     }
   };
-  if constexpr (DEPTH == 3) {
-    // issue order R(tb), DMA(tb), R(tb+1); at each tile the loads younger than its own are the next tile's
-    // register half (LH), so vmcnt(LH) retires this tile's DMA and registers (the last tile: vmcnt(0))
-    i32x4 h0[LH], h1[LH];
-    if (tb < te) {
-      load_hi(h0, tb, lane);
-      dma_lo(tb, 0, lane);
-    }
-    if (tb + 1 < te) load_hi(h1, tb + 1, lane);
-    for (int tile = tb; tile < te; tile += 2) {
-      if (tile + 1 < te) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(LH) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      tile_step(tile, h0, scA, 0);
-      if (tile + 1 < te) {
-        if (tile + 2 < te) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(LH) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        tile_step(tile + 1, h1, scA, 1);
-      }
-    }
-  } else {
-    if (tb < te) load(stgA, scA, tb, lane);
-    if (DEPTH == 2 && tb + 1 < te) load(stgB, scB, tb + 1, lane);
-    for (int tile = tb; tile < te; tile += DEPTH) {
-      tile_step(tile, stgA, scA, 0);
-      if (DEPTH == 2 && tile + 1 < te) tile_step(tile + 1, stgB, scB, 0);
-    }
-  }
+  if (tb < te) load(stgA, scA, tb, lane);
+  for (int tile = tb; tile < te; ++tile) tile_step(tile, stgA, scA);
   l_run += __shfl_xor(l_run, 32, 64);
   if (valid) {
     const float inv = 1.0f / l_run;
@@ -565,8 +483,9 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
 
 template <int QW, int NW, int DEPTH, bool F8 = false, int ABL = 0, bool CAP = false>
 __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
+  static_assert(DEPTH == 1, "one tile staged ahead (the other staging forms are retired: DESIGN.md §6)");
   constexpr int LDR = xldr(QW);
-  constexpr int IMGR = DEPTH == 3 ? 48 : 32;
+  constexpr int IMGR = 32;
   __shared__ __attribute__((aligned(16))) char smem[NW * IMGR * LDR * 2 + (NW + 1) * 16 * 64 * 4 + (F8 ? NW * 32 * 4 : 0)];
   const int n_tiles = (a.T + 31) / 32;
   // XCD-aware item order: the blocks of one (group, split), i.e. its m-tiles, run on one XCD at about the
@@ -761,6 +680,60 @@ void launch_xquant8(const bf16* enc, long long rows, int d, unsigned char* out, 
 }
 
 // ------------------------------------------------------------------------------------------------------
+// Tile-blocked encoder-output slots (the bf16 factored form): slot s holds [n_tiles][NW][32][QW] bf16, n_tiles =
+// ceil(T / 32), rows past T zero; tile t, wave w's block is rows 32 t .. 32 t + 31, columns w QW .. w QW + QW - 1 of
+// the window's [T][d] encoder output, row-major inside the block.  xblock_kernel writes it from row-major windows,
+// xunblock_kernel reads windows back out (the alignment pass's K/V projection).  One thread per 16-B chunk.
+void xattn_geometry(int d, int& qw, int& nw) {
+  switch (d) {
+    case 384: qw = 96; nw = 4; return;
+    case 512: qw = 64; nw = 8; return;
+    case 768: qw = 96; nw = 8; return;
+    case 1024: qw = 128; nw = 8; return;
+    case 1280: qw = 160; nw = 8; return;
+    default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
+  }
+}
+
+long long xblock_slot_elems(int T, int d) { return (long long)((T + 31) / 32) * 32 * d; }
+
+__global__ __launch_bounds__(256) void xblock_kernel(const bf16* __restrict__ src, int B, int T, int d, int qw, int nw,
+                                                     bf16* __restrict__ dst, int to_blocked) {
+  const int cpr = qw / 8, nt = (T + 31) / 32;
+  const long long per = (long long)nt * 32 * d / 8;         // 16-B chunks per blocked slot
+  const long long n = per * B;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n; q += (long long)gridDim.x * 256) {
+    const long long b = q / per;
+    long long rem = q - b * per;
+    const int c = (int)(rem % cpr);
+    rem /= cpr;
+    const int r = (int)(rem % 32);
+    rem /= 32;
+    const int w = (int)(rem % nw);
+    const int t = (int)(rem / nw) * 32 + r;
+    const long long rm = ((long long)b * T + t) * d + w * qw + c * 8;     // row-major element offset
+    if (to_blocked) {
+      i32x4 v = i32x4{0, 0, 0, 0};
+      if (t < T) v = *(const i32x4*)(src + rm);
+      *(i32x4*)(dst + q * 8) = v;
+    } else if (t < T) {
+      *(i32x4*)(dst + rm) = *(const i32x4*)(src + q * 8);
+    }
+  }
+}
+
+// B row-major windows [B][T][d] -> B blocked slots starting at dst (to_blocked), or back (from blocked slots)
+void launch_xblock(const bf16* src, int B, int T, int d, bf16* dst, bool to_blocked, hipStream_t st) {
+  if (B <= 0) return;
+  int qw = 0, nw = 0;
+  xattn_geometry(d, qw, nw);
+  const long long n = (long long)B * xblock_slot_elems(T, d) / 8;
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 1 << 16);
+  hipLaunchKernelGGL(xblock_kernel, dim3(blocks), dim3(256), 0, st, src, B, T, d, qw, nw, dst, to_blocked ? 1 : 0);
+  WM_LAUNCH_CHECK("xblock_kernel");
+}
+
+// ------------------------------------------------------------------------------------------------------
 // host launchers
 
 void launch_xpack(const bf16* ckv_w, bf16* wkt, bf16* wvb, int L, int H, int d, hipStream_t st) {
@@ -829,10 +802,6 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
   a.slab_rows = slab_rows; a.part_u = part_u; a.part_ml = part_ml;
   a.probs = probs; a.head_map = head_map; a.n_align = n_align; a.stat = stat; a.abl = g_xattn_abl;
   const dim3 grid(a.per_xcd * 8);
-  static const int form = [] {
-    const char* e = std::getenv("VLOG_AMD_XFORM");
-    return e ? std::atoi(e) : 0;
-  }();
 #define XA_LAUNCH_C(QW_, NW_, DP_, F8_, CAP_)                                                                      \
   if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_, 0, CAP_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a); \
   else hipLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_, 0, CAP_>), grid, dim3(NW_ * 64), 0, st, a);
@@ -866,20 +835,15 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
     WM_LAUNCH_CHECK("xattn_kernel");
     return;
   }
-  // form 0 (default): 8 waves x d/8 columns, one tile staged ahead (80 KB of E in flight per CU);
-  // form 1 (VLOG_AMD_XFORM=1, experiment): 4 waves x d/4 columns, two tiles ahead (160 KB), which needs
-  // more than the 256 architectural VGPRs per lane at d >= 1024 (spills)
+  // 8 waves x d/8 columns (4 x d/4 at d = 384), one tile staged ahead: 80 KB of E in flight per CU at d = 1280
+  // (retired forms, DESIGN.md §6: 4 waves two tiles ahead, 10 waves x 128 columns, LDS-DMA split staging, and
+  // block-shared images fed by whole-row loads: each slower in the step)
   switch (d) {
-    case 384: if (form) { XA_LAUNCH(96, 4, 2); } else { XA_LAUNCH(96, 4, 1); } break;
-    case 512: if (form) { XA_LAUNCH(128, 4, 2); } else { XA_LAUNCH(64, 8, 1); } break;
-    case 768: if (form) { XA_LAUNCH(192, 4, 2); } else { XA_LAUNCH(96, 8, 1); } break;
-    case 1024: if (form) { XA_LAUNCH(256, 4, 2); } else { XA_LAUNCH(128, 8, 1); } break;
-    case 1280:
-      if (form == 2) { XA_LAUNCH(128, 10, 2); }          // 10 waves x 128 columns, two tiles staged ahead
-      else if (form == 3) { XA_LAUNCH(160, 8, 3); }      // split staging: rows 0-15 by LDS-DMA, 16-31 two ahead
-      else if (form) { XA_LAUNCH(320, 4, 2); }
-      else { XA_LAUNCH(160, 8, 1); }
-      break;
+    case 384: XA_LAUNCH(96, 4, 1); break;
+    case 512: XA_LAUNCH(64, 8, 1); break;
+    case 768: XA_LAUNCH(96, 8, 1); break;
+    case 1024: XA_LAUNCH(128, 8, 1); break;
+    case 1280: XA_LAUNCH(160, 8, 1); break;
     default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
   }
 #undef XA_LAUNCH

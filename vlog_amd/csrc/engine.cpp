@@ -48,6 +48,8 @@ void launch_xpack(const bf16*, bf16*, bf16*, int, int, int, hipStream_t);
 void launch_xq(const bf16*, long long, const CrossFuse&, const bf16*, bf16*, int, int, int, hipStream_t);
 int xattn_splits(int, int, int, int, int);
 void launch_xquant8(const bf16*, long long, int, unsigned char*, float*, hipStream_t);
+long long xblock_slot_elems(int T, int d);
+void launch_xblock(const bf16* src, int B, int T, int d, bf16* dst, bool to_blocked, hipStream_t st);
 void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int, int, int,
                   bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, const float*, const int*, const int*, bf16*,
@@ -829,7 +831,8 @@ void reserve(wm_engine* e, int n_slots, int n_hyp) {
     e->xenc.release();
     e->xscale.release();
     if (e->cross_mode == 1) {
-      e->xenc.ensure((size_t)n_slots * T * m.n_state * (e->cross_fp8 ? 1 : 2));
+      // bf16: tile-blocked slots (attn_xenc.hip xblock_kernel), T padded to whole 32-row tiles
+      e->xenc.ensure(e->cross_fp8 ? (size_t)n_slots * T * m.n_state : (size_t)n_slots * xblock_slot_elems(T, m.n_state) * 2);
       if (e->cross_fp8) e->xscale.ensure((size_t)n_slots * T * 4);
     } else {
       e->ckv.ensure((size_t)L * 2 * n_slots * H * T * 64 * 2);
@@ -1614,9 +1617,9 @@ void forward(wm_engine* e, int n_seq, const int* h_slots, int S, const int* h_to
     const size_t per = (size_t)T * d;
     e->a_enc.ensure((size_t)n_seq * per * 2);
     e->a_kv.ensure((size_t)2 * n_seq * per * 2);
+    const size_t bper = (size_t)xblock_slot_elems(T, d);
     for (int s = 0; s < n_seq; ++s)
-      HIP_OK(hipMemcpyAsync(e->a_enc.as<bf16>() + (size_t)s * per, e->xenc.as<bf16>() + (size_t)hs[s] * per, per * 2,
-                            hipMemcpyDeviceToDevice, st));
+      launch_xblock(e->xenc.as<bf16>() + (size_t)hs[s] * bper, 1, T, d, e->a_enc.as<bf16>() + (size_t)s * per, false, st);
     e->tf_nwin = n_seq;
   }
   struct TfReset { wm_engine* e; ~TfReset() { e->tf_nwin = 0; } } tf_reset{e};
@@ -2344,11 +2347,11 @@ int wm_cross_kv(wm_engine* e, const void* d_enc, int32_t B, int32_t slot0, void*
                      e->xscale.as<float>() + (size_t)slot0 * T, (hipStream_t)stream);
       return;
     }
-    if (e->cross_mode == 1) {   // factored: the slot holds the encoder output itself
+    if (e->cross_mode == 1) {   // factored: the slot holds the encoder output itself, tile-blocked
       const size_t per = (size_t)T * d;
       ProfScope ps(e, P_CROSSKV_GEMM, (hipStream_t)stream, 0, 2.0 * 2 * B * per);
-      HIP_OK(hipMemcpyAsync(e->xenc.as<bf16>() + (size_t)slot0 * per, d_enc, (size_t)B * per * 2,
-                            hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      launch_xblock((const bf16*)d_enc, B, T, d, e->xenc.as<bf16>() + (size_t)slot0 * xblock_slot_elems(T, d), true,
+                    (hipStream_t)stream);
       return;
     }
     GemmEpi ep = epi_of(EPI_CROSS_KV, e->ckv.p, 0, e->Wf("dec.ckv.b"));
