@@ -214,6 +214,8 @@ struct wm_engine {
   int dec_big128 = 0;        // ... from this many rows qkv / fc1 / fc2 in 128-row groups (0: never; VLOG_AMD_DEC_BIG128).
                              // Off: faster alone (dec_gemm_bench, 750 rows) but slower in the step (config 5, arms
                              // alternating on one box: dec_gemm 605 vs 566 ms per step, profiles/ab_r04_c5_big128.txt)
+  int dec_ln_fold = 1;       // ring passes (33..1024 rows): LayerNorms folded into their consumers (no combine launch
+                             // after out / cout; fc2's combine writes stats instead of the LayerNorm)
   int dec_big_lds = 72;      // ... qkv / fc1 / fc2 with this LDS budget per ring block (KiB): 72 = two resident blocks
                              // per CU (tools/dec_gemm_bench at 750 rows: qkv 24.7 -> 18.8 us, fc1 31.3 -> 21.4, fc2
                              // 41.6 -> 33.1 against 144; at 256 rows qkv+fc1+fc2 45.6 -> 35.7 us per layer against the
@@ -227,6 +229,11 @@ struct wm_engine {
   DevBuf xwkt;               // factored: Wk^T per layer and head [L][H][d][64] bf16, packed from dec.ckv.w
   DevBuf xwvb;               // factored: Wv per layer and head in 16-column blocks [L][H][d/16][64][16]
   bool xwkt_ready = false;
+  // folded LayerNorm (decode_ln_fold): per decoder layer s = W g and c = W b + bias of qkv (ln1), cq (ln2), fc1 (ln3),
+  // [L][qkv_s 3d | qkv_c 3d | cq_s d | cq_c d | fc1_s 4d | fc1_c 4d] f32, computed once per weight upload
+  DevBuf fold_vec;
+  bool fold_ready = false;
+  DevBuf fold_stat[2];       // producer row sums per decode slice: [d/16][rows][2]
   DevBuf s_qp, s_pu, s_pml;  // factored step scratch: q' [rows][H][d], split partials u/l and (m, l)
   int cross_cap = 0;         // cross-attention grid cap (0: one block per item; >0: persistent grid-stride form,
                              // 2 blocks/CU measured ~2 % faster alone but slower with the fused q combine)
@@ -561,7 +568,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     ProfScope ps(e, P_DEC_GEMM, st, 2.0 * rows * N * K, gemm_bytes(rows, N, K, ob));
     // one window's beam (or a handful of rows): the weight-streaming small-M kernel
     if (sl.total_rows <= 32 && e->dec_gemv && launch_dec_gemv(a, w, ldw, rows, N, K, ep, ws, wsb, st)) return;
-    if (a.lnx || ep.stat_out) throw std::runtime_error("decoder: fused LayerNorm operand off the small-M path");
+    if (a.lnx || (ep.stat_out && !ep.xg_out)) throw std::runtime_error("decoder: fused LayerNorm operand off the small-M path");
     // passes of >= dec_big_rows rows (beam groups of many windows; tools/dec_gemm_bench at 384 and 750 rows): 64-row
     // ring groups; 64 columns for qkv and fc1, and for every projection from 512 rows; fc2's whole K per block
     // (384 rows: 76 vs 86 us per layer for the 150-row plan; 750 rows: 114 vs 159 us)
@@ -582,6 +589,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols, lds)) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
+    if (a.fold_stat || ep.xg_out) throw std::runtime_error("decoder: a folded-LayerNorm projection left the ring path");
     launch_gemm(a, w, ldw, rows, N, K, ep, ws, wsb, st);
   };
   // residual-producing GEMMs also apply the LayerNorm that consumes the residual (EPI_RESID_LN: fused into
@@ -612,20 +620,66 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   // fc2 -> the next layer's ln1 the same way: fc2 (K = 4d) writes the residual and its statistics without split-K,
   // the next layer's qkv normalises its operand (the same for every layer of a pass, so layer l > 0's qkv knows)
   const bool fc2_fuse = ln_fuse && e->dec_gemv_ln_fc2 && gemv_ln_fusable(rows, d, 4 * d, d);
+  // Folded LayerNorms (ring passes): the residual producers (out, cout, fc2) write x, bf16(x * g) into hb and row
+  // sums; the consumers (cq, fc1, next qkv) multiply hb and finish the LayerNorm in their epilogue (gemm.h GemmA
+  // fold_*), so out and cout need no combine launch and fc2's combine writes sums instead of the LayerNorm.  Only
+  // where every projection of the layer takes the ring path with the consumers' whole K per block.
+  const int trows = sl.total_rows;
+  const bool big_route = e->dec_big_rows > 0 && trows >= e->dec_big_rows && trows <= 1024;
+  auto ring_route = [&](int proj, int K) {
+    if (trows <= 32 && e->dec_gemv) return false;
+    if (big_route) return true;
+    const int p = plan_of(proj);
+    return p > 0 || (p == 0 && e->dec_ring && K <= 1280 && trows <= 160);
+  };
+  const bool fold = e->dec_ln_fold && e->fold_ready && !ln_fuse && trows > 32 && trows <= 1024 && !(attn && align_map) &&
+                    ring_route(DEC_QKV, d) && ring_route(DEC_OUT, d) && ring_route(DEC_CQ, d) && ring_route(DEC_COUT, d) &&
+                    ring_route(DEC_FC1, d) && ring_route(DEC_FC2, 4 * d) && e->dec_kr[DEC_QKV] == 0 &&
+                    e->dec_kr[DEC_CQ] == 0 && e->dec_kr[DEC_FC1] == 0 && d % 16 == 0;
+  float* fstat = nullptr;
+  const float* fv = nullptr;
+  if (fold) {
+    DevBuf& fb = e->fold_stat[r0 == 0 ? 0 : 1];
+    fb.ensure((size_t)(d / 16) * rows * 2 * 4);
+    fstat = fb.as<float>();
+    fv = e->fold_vec.as<float>() + (size_t)l * 16 * d;
+  }
+  auto fold_producer = [&](const float* bias, const float* g_next) {
+    GemmEpi ep = epi_of(EPI_RESID_F32, x, d, bias);
+    ep.stat_out = fstat; ep.xg_out = hb; ep.xg_g = g_next; ep.xg_ld = d;
+    return ep;
+  };
+  auto fold_operand = [&](int tiles) {
+    GemmA a = amat(hb, d);
+    a.fold_stat = fstat; a.fold_tiles = tiles; a.fold_rows = rows;
+    return a;
+  };
+  auto fold_epi = [&](GemmEpi ep, size_t off, int N) {
+    ep.bias = nullptr;
+    ep.fold_s = fv + off; ep.fold_c = fv + off + N;
+    return ep;
+  };
+  // fc2's K ranges as the gemm route picks them (the same for every layer of the pass): split-K slabs -> its combine
+  // writes one whole-row tile of sums; one range -> the ring epilogue writes d / 16 tiles (read by the next qkv)
+  const int fc2_kr = e->dec_kr[DEC_FC2] > 0 ? std::min(e->dec_kr[DEC_FC2], 4 * d) : (4 * d <= 1280 || big_route ? 4 * d : 1280);
+  const int fc2_tiles = (4 * d + fc2_kr - 1) / fc2_kr > 1 ? 1 : d / 16;
+  const bool fold_qkv = fold && l > 0;
   bf16* kc = skv + (size_t)(2 * l) * skv_layer;
   bf16* vc = skv + (size_t)(2 * l + 1) * skv_layer;
   {
     GemmEpi ep = epi_of(EPI_DEC_QKV, q, d, W.qkv_b);
     ep.kcache = kc; ep.vcache = vc; ep.row_hyp = row_hyp; ep.row_pos = row_pos;
     ep.d = d; ep.n_head = H; ep.head_dim = 64; ep.n_ctx = C;
-    gemm(DEC_QKV, (fc2_fuse && l > 0) ? ln_operand(W.ln1_w, W.ln1_b) : amat(hb, d), W.qkv_w, d, 3 * d, d, ep);
+    if (fold_qkv) gemm(DEC_QKV, fold_operand(fc2_tiles), W.qkv_w, d, 3 * d, d, fold_epi(ep, 0, 3 * d));
+    else gemm(DEC_QKV, (fc2_fuse && l > 0) ? ln_operand(W.ln1_w, W.ln1_b) : amat(hb, d), W.qkv_w, d, 3 * d, d, ep);
   }
   {
     ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
     launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b,
                      sl.total_rows);
   }
-  gemm(DEC_OUT, amat(ao, d), W.out_w, d, d, d, ln_fuse ? resid_stat(W.out_b) : resid_ln(W.ln2_w, W.ln2_b, W.out_b));
+  gemm(DEC_OUT, amat(ao, d), W.out_w, d, d, d,
+       fold ? fold_producer(W.out_b, W.ln2_w) : ln_fuse ? resid_stat(W.out_b) : resid_ln(W.ln2_w, W.ln2_b, W.out_b));
   // cq: when the skinny split-K path runs it and no attention is captured, its slabs stay in the scratch and
   // the cross-attention kernel sums them while loading q (no combine launch)
   CrossFuse fz;
@@ -640,7 +694,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
       ep.defer_combine = 1;
       fz.q_part = ws; fz.q_splits = sk; fz.q_rows = rows; fz.q_bias = W.cq_b;
     }
-    gemm(DEC_CQ, ln_fuse ? ln_operand(W.ln2_w, W.ln2_b) : amat(hb, d), W.cq_w, d, d, d, ep);
+    if (fold) gemm(DEC_CQ, fold_operand(d / 16), W.cq_w, d, d, d, fold_epi(ep, 6 * (size_t)d, d));
+    else gemm(DEC_CQ, ln_fuse ? ln_operand(W.ln2_w, W.ln2_b) : amat(hb, d), W.cq_w, d, d, d, ep);
   }
   if ((e->cross_fuse & 2) && e->cross_mode == 0) fz.cnt = e->d_cross_cnt.as<int>() + (size_t)r0 * H;
   fz.tf = (attn && align_map && e->cross_tf) ? 1 : 0;
@@ -708,16 +763,22 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
                       e->cross_cap, fz, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
   }
   if (probs) HIP_OK(hipStreamSynchronize(st));   // the head map buffer is reused by the next layer
-  gemm(DEC_COUT, amat(ao, d), W.cout_w, d, d, d, ln_fuse ? resid_stat(W.cout_b) : resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
+  gemm(DEC_COUT, amat(ao, d), W.cout_w, d, d, d,
+       fold ? fold_producer(W.cout_b, W.ln3_w) : ln_fuse ? resid_stat(W.cout_b) : resid_ln(W.ln3_w, W.ln3_b, W.cout_b));
   {
     GemmEpi ep = epi_of(EPI_BF16, ff, 4LL * d, W.fc1_b);
     ep.act = 1;
-    gemm(DEC_FC1, ln_fuse ? ln_operand(W.ln3_w, W.ln3_b) : amat(hb, d), W.fc1_w, d, 4 * d, d, ep);
+    if (fold) gemm(DEC_FC1, fold_operand(d / 16), W.fc1_w, d, 4 * d, d, fold_epi(ep, 8 * (size_t)d, 4 * d));
+    else gemm(DEC_FC1, ln_fuse ? ln_operand(W.ln3_w, W.ln3_b) : amat(hb, d), W.fc1_w, d, 4 * d, d, ep);
   }
   if (l + 1 < L) {
     const auto& Wn = dec_weights(e)[l + 1];
-    gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d,
-         fc2_fuse ? resid_stat(W.fc2_b) : resid_ln(Wn.ln1_w, Wn.ln1_b, W.fc2_b));
+    if (fold) {
+      gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, fold_producer(W.fc2_b, Wn.ln1_w));
+    } else {
+      gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d,
+           fc2_fuse ? resid_stat(W.fc2_b) : resid_ln(Wn.ln1_w, Wn.ln1_b, W.fc2_b));
+    }
   } else {
     gemm(DEC_FC2, amat(ff, 4LL * d), W.fc2_w, 4LL * d, d, 4 * d, epi_of(EPI_RESID_F32, x, d, W.fc2_b));
   }
@@ -762,6 +823,18 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
       e->xwkt_ready = true;
     }
     if (!e->xenc.p) throw std::runtime_error("decoder: no encoder slots (wm_reserve + wm_cross_kv first)");
+  }
+  if (e->dec_ln_fold && !e->fold_ready) {
+    const int L2 = m.n_dec_layer;
+    e->fold_vec.ensure((size_t)L2 * 16 * d * 4);
+    for (int l = 0; l < L2; ++l) {
+      const auto& W = dec_weights(e)[l];
+      float* f = e->fold_vec.as<float>() + (size_t)l * 16 * d;
+      launch_fold_vectors(W.qkv_w, 3 * d, d, W.ln1_w, W.ln1_b, W.qkv_b, f, f + 3 * d, st);
+      launch_fold_vectors(W.cq_w, d, d, W.ln2_w, W.ln2_b, W.cq_b, f + 6 * d, f + 7 * d, st);
+      launch_fold_vectors(W.fc1_w, 4 * d, d, W.ln3_w, W.ln3_b, W.fc1_b, f + 8 * d, f + 12 * d, st);
+    }
+    e->fold_ready = true;
   }
   int h0 = (rows / 2 / cross_group) * cross_group;
   const bool split = e->dec_split && logit_rows == nullptr && n_logit == rows && attn == nullptr && h0 >= 16 &&
@@ -2173,6 +2246,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_DEC_GEMV")) e->dec_gemv = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_GEMV_LN")) e->dec_gemv_ln = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_RING")) e->dec_ring = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_DEC_LN_FOLD")) e->dec_ln_fold = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_PLAN")) {
       const int p = std::atoi(v) != 0;
       for (int i = 0; i < DEC_NPROJ; ++i) e->dec_plan[i] = kDecPlanPresets[p][i], e->dec_cols[i] = kDecColsPresets[p][i];
@@ -2255,6 +2329,7 @@ int wm_set_weight(wm_engine* e, const char* name, const void* d_src, int64_t nby
     HIP_OK(hipMemcpyAsync((char*)e->arena.p + it->second.off, d_src, nbytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     it->second.set = true;
     if (it->first == "dec.ckv.w") e->xwkt_ready = false;
+    e->fold_ready = false;
   });
 }
 
@@ -2539,6 +2614,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_mfma") e->cross_mfma = value ? 1 : 0;
     else if (k == "cross_mfma_fuse") e->cross_mfma_fuse = value ? 1 : 0;
     else if (k == "decode_gemm_big_rows") e->dec_big_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
+    else if (k == "decode_ln_fold") e->dec_ln_fold = value ? 1 : 0;
     else if (k == "decode_gemm_big_lds") {
       if (value != 72 && value != 144) throw std::runtime_error("decode_gemm_big_lds: 72 or 144");
       e->dec_big_lds = (int)value;
@@ -2586,6 +2662,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_mfma") *value = e->cross_mfma;
     else if (k == "cross_mfma_fuse") *value = e->cross_mfma_fuse;
     else if (k == "decode_gemm_big_rows") *value = e->dec_big_rows;
+    else if (k == "decode_ln_fold") *value = e->dec_ln_fold;
     else if (k == "decode_gemm_big_lds") *value = e->dec_big_lds;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
   });

@@ -15,6 +15,15 @@ struct GemmA {
   const float* ln_b;
   const float* ln_stat;
   int ln_tiles;
+  // ring path only (launch_dec_ring), the folded LayerNorm: the operand rows hold bf16(x * g) (written by the
+  // residual producer, GemmEpi.xg_out) and the row statistics are the producer's partial sums fold_stat
+  // (sum x, sum x^2 per tile).  The kernel forms mean and rstd per row and its epilogue
+  // applies y = rstd * acc - rstd * mean * fold_s[n] + fold_c[n] (GemmEpi) before the epilogue kind (fold_stat is
+  // [fold_rows][fold_tiles][2]: 1 tile, or an even count <= 80):
+  // W . LN(x) + bias = rstd (W . (g x)) - rstd mean (W g) + (W b + bias).
+  const float* fold_stat;
+  int fold_tiles;
+  long long fold_rows;
 };
 
 // Epilogue kinds (see gemm.hip for the exact formulas)
@@ -50,8 +59,13 @@ struct GemmEpi {
   // that sums them itself (see skinny_splits)
   int defer_combine;
   // small-M path only, EPI_RESID_F32 without split-K: per (16-column tile, row) sums of the updated residual
-  // (sum x, sum x^2) [N/16][M][2] for a LayerNorm-consuming GEMM (GemmA.lnx)
+  // (sum x, sum x^2) [N/16][M][2] for a LayerNorm-consuming GEMM (GemmA.lnx).  Ring path / split-K combine of an
+  // EPI_RESID_F32 producer with xg_out set: the sums as [M][N/16][2] (ring) or [M][1][2] (the split-K combine)
+  // plus xg_out[r][c] = bf16(x[r][c] * xg_g[c]) (the next LayerNorm's gamma) for a folded consumer (GemmA.fold_*)
   float* stat_out;
+  bf16* xg_out; const float* xg_g; long long xg_ld;
+  // folded-LayerNorm consumer (GemmA.fold_stat): W g and W b + bias per output column (bias is then nullptr)
+  const float* fold_s; const float* fold_c;
 };
 
 // Split count the skinny path would use for this shape (>= 1), or 0 when launch_gemm would not take it.
@@ -82,6 +96,9 @@ void launch_splitk_combine(const float* part, int splitk, int M, int N, const Ge
 // LDS budget, 144 (one block per CU) or 72 (two resident blocks per CU); 0 = the process default (VLOG_AMD_RING_LDS).
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      size_t ws_bytes, int kr, hipStream_t st, int rows_per_block = 0, int cols = 32, int lds_kb = 0);
+// Folded-LayerNorm vectors of a consumer projection (gemm_dec.hip): s = W g, c = W b + bias (f64 sums, f32 out).
+void launch_fold_vectors(const bf16* w, int N, int K, const float* g, const float* b, const float* bias, float* s_out,
+                         float* c_out, hipStream_t st);
 // One-shot decoder-row path (gemm_dec.hip): 32 rows x nc*16 columns per 512-thread block, every load of a
 // <= 1280-deep K range issued at once into MFMA operand registers, per-wave K split summed through LDS.
 bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,

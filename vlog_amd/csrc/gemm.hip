@@ -244,6 +244,9 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmA a, const bf16* __rest
 // loads in flight (150 decoder rows cannot fill the chip, so latency, not bandwidth, is the cost).
 // x[r] += sum_s part[s][r] + bias;  ln_out[r] = LN(x[r]) (two-pass mean / variance, eps 1e-5).  Summation
 // order per element = splitk_reduce_kernel's.
+// FOLD (a folded-LayerNorm consumer follows, GemmEpi.xg_out): instead of the LayerNorm, the row's sums (sum x,
+// sum x^2) go to stat_out[r] (one tile per row) and xg_out[r] = bf16(x[r] * xg_g).
+template <bool FOLD>
 __global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __restrict__ part, int splitk, int M, int N,
                                                                GemmEpi epi) {
   __shared__ float red[2][16];
@@ -258,7 +261,8 @@ __global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __re
   float2* xr = (float2*)((float*)epi.out + (long long)r * epi.ldc);
   const float2 x0 = xr[cc];
   const float2 bias2 = epi.bias ? ((const float2*)epi.bias)[cc] : make_float2(0.f, 0.f);
-  const float2 gg = ((const float2*)epi.ln_g)[cc], lb = ((const float2*)epi.ln_b)[cc];
+  const float2 gg = ((const float2*)(FOLD ? epi.xg_g : epi.ln_g))[cc];
+  const float2 lb = FOLD ? make_float2(0.f, 0.f) : ((const float2*)epi.ln_b)[cc];
   float2 acc = make_float2(0.f, 0.f);
 #pragma unroll 8
   for (int sp = 0; sp < splitk; ++sp) {
@@ -278,6 +282,31 @@ __global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __re
     xr[c] = xv;
     acc = xv;
     s = xv.x + xv.y;
+  }
+  if constexpr (FOLD) {
+    float q2 = act ? acc.x * acc.x + acc.y * acc.y : 0.f;
+    s = wave_sum(s);
+    q2 = wave_sum(q2);
+    if (lane == 0) {
+      red[0][wid] = s;
+      red[1][wid] = q2;
+    }
+    if (act) {
+      bf16x2 o;
+      o[0] = f2bf(acc.x * gg.x);
+      o[1] = f2bf(acc.y * gg.y);
+      ((bf16x2*)(epi.xg_out + (long long)r * epi.xg_ld))[c] = o;
+    }
+    __syncthreads();
+    if (c == 0) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int i = 0; i < nw; ++i) {
+        t1 += red[0][i];
+        t2 += red[1][i];
+      }
+      *(float2*)(epi.stat_out + 2LL * r) = make_float2(t1, t2);
+    }
+    return;
   }
   s = wave_sum(s);
   if (lane == 0) red[0][wid] = s;
@@ -307,13 +336,14 @@ __global__ __launch_bounds__(1024) void resid_ln_reduce_kernel(const float* __re
 static void launch_resid_ln_reduce(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st) {
   if (N % 2 != 0 || N > 2048) throw std::runtime_error("resid_ln_reduce: unsupported width " + std::to_string(N));
   const int threads = ((N / 2 + 63) / 64) * 64;
-  hipLaunchKernelGGL(resid_ln_reduce_kernel, dim3(M), dim3(threads), 0, st, part, splitk, M, N, epi);
+  if (epi.kind == EPI_RESID_F32) hipLaunchKernelGGL((resid_ln_reduce_kernel<true>), dim3(M), dim3(threads), 0, st, part, splitk, M, N, epi);
+  else hipLaunchKernelGGL((resid_ln_reduce_kernel<false>), dim3(M), dim3(threads), 0, st, part, splitk, M, N, epi);
   WM_LAUNCH_CHECK("resid_ln_reduce_kernel");
 }
 
 // Deterministic combine of `splitk` partial slabs [splitk][M][N] + the epilogue (used by gemm_dec.hip).
 void launch_splitk_combine(const float* part, int splitk, int M, int N, const GemmEpi& epi, hipStream_t st) {
-  if (epi.kind == EPI_RESID_LN) {
+  if (epi.kind == EPI_RESID_LN || (epi.kind == EPI_RESID_F32 && epi.xg_out)) {
     launch_resid_ln_reduce(part, splitk, M, N, epi, st);
     return;
   }

@@ -150,6 +150,10 @@ bool launch_dec_gemm(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if ((size_t)mf * 16 * KR * 2 > 150 * 1024) return false;      // A panels must fit in LDS
   const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
+  // folded LayerNorm: a consumer needs the stat rows of its pass; a producer writes whole 16-column tiles
+  if (a.fold_stat && (!(a.fold_tiles == 1 || (a.fold_tiles % 2 == 0 && a.fold_tiles <= 80)) || a.fold_rows < M || epi.bias ||
+                      !epi.fold_s || !epi.fold_c || slab)) return false;
+  if (epi.xg_out && (epi.kind != EPI_RESID_F32 || N % 16 != 0 || !epi.stat_out || !epi.bias || !epi.xg_g)) return false;
   switch (epi.kind) {
     case EPI_BF16: dispatch_mf<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, KR, splitk, st); break;
     case EPI_RESID_F32: dispatch_mf<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, KR, splitk, st); break;
@@ -191,6 +195,7 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   constexpr int ROWS = MF * 16, HALF = MF / 2, WR = 32 * NC, SUB = (ROWS + WR) * 64, SLOT = PK * SUB, DA = ROWS / 32,
                 DPP = PK * (DA + NC);
   __shared__ __attribute__((aligned(16))) bf16 smem[R * SLOT];
+  __shared__ float sMR[2][ROWS];                        // folded LayerNorm: rstd and rstd * mean per row
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -201,7 +206,26 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   const int kb = split * kr, klen = min(kr, K - kb), NS = klen / 64, NP = (NS + PK - 1) / PK;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid & 1, wr = wid >> 1;
-
+  // folded LayerNorm (a.fold_stat): the row sums [M][tiles][2] of the block's rows are requested BEFORE the ring's
+  // first panels and reduced after them, so their round trip overlaps the DMA latency; 8 threads per row, thread p
+  // summing 16-B pairs of tiles p, p + 8, ... in order, then a fixed xor tree (every block forms the same bits)
+  constexpr int FCH = (ROWS + 31) / 32, FQ = 5;                  // 32-row chunks; up to 80 tiles = 40 pairs
+  f32x4 fq[FCH][FQ];
+  const bool fold = a.fold_stat != nullptr;
+  if (fold) {
+    const int T = a.fold_tiles, part = tid & 7;
+#pragma unroll
+    for (int ch = 0; ch < FCH; ++ch) {
+      const int gr = min(m0 + ch * 32 + (tid >> 3), M - 1);
+      const float* sr = a.fold_stat + (long long)gr * T * 2;
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) {
+        const int q = part + 8 * j;
+        if (T == 1) fq[ch][j] = (j == 0 && part == 0) ? f32x4{sr[0], sr[1], 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
+        else fq[ch][j] = 2 * q < T ? *(const f32x4*)(sr + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
   // DMA sources: wave `wid` moves A rows [wid*ROWS/4, +ROWS/4) (DA instructions of 8 rows) and W rows
   // [8 NC wid, +8 NC) (NC instructions)
   const bf16* srcA[DA];
@@ -244,6 +268,31 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
     for (int i = 0; i < HALF; ++i) acc[c][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int pre = min(R - 1, NP);
   for (int p = 0; p < pre; ++p) issue(p);
+  if (fold) {
+#pragma unroll
+    for (int ch = 0; ch < FCH; ++ch) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) {
+        s1 += fq[ch][j][0] + fq[ch][j][2];
+        s2 += fq[ch][j][1] + fq[ch][j][3];
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      const int rr = ch * 32 + (tid >> 3);
+      if ((tid & 7) == 0 && rr < ROWS) {
+        const float mean = s1 / (float)K, var = fmaxf(s2 / (float)K - mean * mean, 0.f);
+        const float rs = rsqrtf(var + 1e-5f);
+        sMR[0][rr] = rs;
+        sMR[1][rr] = rs * mean;
+      }
+    }
+    // LDS only: the DMAs in flight are not waited for (a workgroup fence would drain vmcnt)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   for (int p = 0; p < NP; ++p) {
     vm_wait(min(NP - 1 - p, R - 2) * DPP);            // this wave's DMAs of super-panel p have landed
     asm volatile("s_barrier" ::: "memory");           // ... everyone's; slot of super-panel p-1 is free
@@ -279,15 +328,49 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int col0 = n0 + (wc * NC + c) * 16 + 4 * (lane >> 4);
-    if (col0 >= N) continue;
 #pragma unroll
     for (int i = 0; i < HALF; ++i) {
-      const int row = m0 + (wr * HALF + i) * 16 + (lane & 15);
-      if (row >= M) continue;
-      if (to_slab)
+      const int lr = (wr * HALF + i) * 16 + (lane & 15), row = m0 + lr;
+      // residual producer for a folded LayerNorm (uniform over the block; N % 16 == 0): the updated residual, its
+      // bf16(x * g) operand image and the per-(16-column tile, row) sums, the tile's 4 lanes of a row reduced by a
+      // fixed xor tree (every lane takes part: the 4 lanes of a row share its validity)
+      if (KIND == EPI_RESID_F32 && !to_slab && epi.xg_out) {
+        const bool ok = row < M && col0 < N;
+        f32x4 xn = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (ok) {
+          f32x4* px = (f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0);
+          xn = *px + acc[c][i] + *(const f32x4*)(epi.bias + col0);
+          *px = xn;
+          const f32x4 g = *(const f32x4*)(epi.xg_g + col0);
+          bf16x4 xg;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xg[e] = f2bf(xn[e] * g[e]);
+          *(bf16x4*)(epi.xg_out + (long long)row * epi.xg_ld + col0) = xg;
+        }
+        float s1 = (xn[0] + xn[1]) + (xn[2] + xn[3]);
+        float s2 = (xn[0] * xn[0] + xn[1] * xn[1]) + (xn[2] * xn[2] + xn[3] * xn[3]);
+        s1 += __shfl_xor(s1, 16, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (ok && (lane >> 4) == 0)
+          *(float2*)(epi.stat_out + ((long long)row * (N >> 4) + (col0 >> 4)) * 2) = make_float2(s1, s2);
+        continue;
+      }
+      if (col0 >= N || row >= M) continue;
+      if (to_slab) {
         *(f32x4*)(part + ((long long)split * M + row) * N + col0) = acc[c][i];
-      else
+      } else if (a.fold_stat) {
+        // folded LayerNorm consumer: rstd (W . gx) - rstd mean (W g) + (W b + bias), then the epilogue kind
+        const float rs = sMR[0][lr], rm = sMR[1][lr];
+        const f32x4 fs = *(const f32x4*)(epi.fold_s + col0), fc = *(const f32x4*)(epi.fold_c + col0);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[c][i][e], rs, fc[e] - rm * fs[e]);
+        apply_epi4<KIND>(epi, row, col0, v);
+      } else {
         apply_epi4<KIND>(epi, row, col0, acc[c][i]);
+      }
     }
   }
 }
@@ -389,6 +472,10 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if ((K - (splitk - 1) * kr) % 64 != 0) return false;
   const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
+  // folded LayerNorm: a consumer needs the stat rows of its pass; a producer writes whole 16-column tiles
+  if (a.fold_stat && (!(a.fold_tiles == 1 || (a.fold_tiles % 2 == 0 && a.fold_tiles <= 80)) || a.fold_rows < M || epi.bias ||
+                      !epi.fold_s || !epi.fold_c || slab)) return false;
+  if (epi.xg_out && (epi.kind != EPI_RESID_F32 || N % 16 != 0 || !epi.stat_out || !epi.bias || !epi.xg_g)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   switch (epi.kind) {
     case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
@@ -539,6 +626,10 @@ bool launch_dec_oneshot(const GemmA& a, const bf16* w, long long ldw, int M, int
   const int kr = K / splitk;
   const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
+  // folded LayerNorm: a consumer needs the stat rows of its pass; a producer writes whole 16-column tiles
+  if (a.fold_stat && (!(a.fold_tiles == 1 || (a.fold_tiles % 2 == 0 && a.fold_tiles <= 80)) || a.fold_rows < M || epi.bias ||
+                      !epi.fold_s || !epi.fold_c || slab)) return false;
+  if (epi.xg_out && (epi.kind != EPI_RESID_F32 || N % 16 != 0 || !epi.stat_out || !epi.bias || !epi.xg_g)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   switch (epi.kind) {
     case EPI_BF16: dispatch_oneshot<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, nc, st); break;
@@ -837,6 +928,10 @@ bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   }
   const bool slab = splitk > 1 || epi.kind == EPI_RESID_LN;
   if (slab && (!ws || (size_t)splitk * M * N * 4 > ws_bytes)) return false;
+  // folded LayerNorm: a consumer needs the stat rows of its pass; a producer writes whole 16-column tiles
+  if (a.fold_stat && (!(a.fold_tiles == 1 || (a.fold_tiles % 2 == 0 && a.fold_tiles <= 80)) || a.fold_rows < M || epi.bias ||
+                      !epi.fold_s || !epi.fold_c || slab)) return false;
+  if (epi.xg_out && (epi.kind != EPI_RESID_F32 || N % 16 != 0 || !epi.stat_out || !epi.bias || !epi.xg_g)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   if (a.lnx) {
     if (epi.kind == EPI_DEC_QKV) run_gemv_lna<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
@@ -858,4 +953,36 @@ bool launch_dec_gemv(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   }
   if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);
   return true;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Folded-LayerNorm vectors of a consumer projection W [N][K] (bf16, as the GEMM reads it) behind a LayerNorm with
+// affine (g, b): s[n] = sum_k W[n][k] g[k] and c[n] = sum_k W[n][k] b[k] + bias[n], accumulated in f64 in a fixed
+// order (one wave per output column), rounded once to f32.  Run once per weight upload (engine.cpp fold_vectors).
+__global__ __launch_bounds__(256) void fold_vec_kernel(const bf16* __restrict__ w, int N, int K, const float* __restrict__ g,
+                                                       const float* __restrict__ b, const float* __restrict__ bias,
+                                                       float* __restrict__ s_out, float* __restrict__ c_out) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  double s = 0.0, c = 0.0;
+  for (int k = lane; k < K; k += 64) {
+    const double wv = (double)bf2f(w[(long long)n * K + k]);
+    s += wv * (double)g[k];
+    c += wv * (double)b[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if (lane == 0) {
+    s_out[n] = (float)s;
+    c_out[n] = (float)(c + (double)bias[n]);
+  }
+}
+
+void launch_fold_vectors(const bf16* w, int N, int K, const float* g, const float* b, const float* bias, float* s_out,
+                         float* c_out, hipStream_t st) {
+  hipLaunchKernelGGL(fold_vec_kernel, dim3((N + 3) / 4), dim3(256), 0, st, w, N, K, g, b, bias, s_out, c_out);
+  WM_LAUNCH_CHECK("fold_vec_kernel");
 }
