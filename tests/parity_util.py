@@ -138,6 +138,22 @@ def record(name: str, rows: List[WindowParity], **extra) -> dict:
     return out
 
 
+def source_offset(stride: int, env: str) -> int:
+    """Which residue class of windows a strided sweep covers: seeded by the tree's kernel sources (the GPU box has no
+    .git), so every change of the HIP code rotates the swept windows and every window is eventually covered (the
+    environment variable `env` overrides).  Tests record it with their results."""
+    if env in os.environ:
+        return int(os.environ[env]) % stride
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vlog_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(root, "*.hip")) + glob.glob(os.path.join(root, "*.cpp"))):
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return int.from_bytes(h.digest()[:4], "little") % stride
+
+
 def sample_indices(n: int, k: int) -> List[int]:
     """k window indices spread over [0, n), first and last included."""
     if k >= n:

@@ -20,7 +20,7 @@ import torch
 
 from oracle.decode import GenerateOptions, beam_many
 from oracle.model import OracleWhisper
-from tests.parity_util import GATE_IDENTICAL, assert_gates, gate_windows, sample_indices
+from tests.parity_util import GATE_IDENTICAL, assert_gates, gate_windows, sample_indices, source_offset
 from vlog_amd.audio import speech_like
 from vlog_amd.dims import model_dims
 from vlog_amd.tokenizer import Tokenizer
@@ -247,12 +247,13 @@ def test_config4_variable_length_gates_and_row_set_decode(lv3_var):
     # every 3rd window plus the shortest and the longest transcript through the oracle (every window of the uniform
     # config 4 is gated above; VLOG_AMD_GATE_STRIDE=1 gates every window here too)
     stride = max(1, int(os.environ.get("VLOG_AMD_GATE_STRIDE", "3")))
+    offset = source_offset(stride, "VLOG_AMD_GATE_OFFSET")           # rotates with the kernel sources
     lens0 = [len(r.tokens) for r in res]
-    gw = sorted(set(range(0, cfg.W, stride)) | {int(np.argmin(lens0)), int(np.argmax(lens0))})
+    gw = sorted(set(range(offset, cfg.W, stride)) | {int(np.argmin(lens0)), int(np.argmax(lens0))})
     g = gate_windows(cfg.orc, cfg.enc_of, cfg.prompt, res, cfg.st, cfg.opt(), cfg.tok, windows=gw)
     g.pop("oracle_tokens", None)
     _record(f"gates large-v3 variable-length greedy 150 windows ({len(gw)} gated)",
-            {k: v for k, v in g.items()})
+            dict({k: v for k, v in g.items()}, stride=stride, offset=offset))
     assert_gates(g)
     lens = [len(r.tokens) for r in res]
     # the corpus's 150 windows: the 15 room-tone windows decode one token (the quiet bit), the speech windows 44 to

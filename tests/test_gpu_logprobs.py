@@ -28,7 +28,7 @@ import torch
 
 from oracle.decode import GenerateOptions
 from oracle.model import OracleWhisper
-from tests.parity_util import oracle_records, progress, record_deviation
+from tests.parity_util import oracle_records, progress, record_deviation, source_offset
 from vlog_amd.audio import speech_like
 from vlog_amd.dims import model_dims
 from vlog_amd.tokenizer import Tokenizer
@@ -39,9 +39,13 @@ pytestmark = pytest.mark.gpu
 BAR = 0.02          # nats, bf16 engine vs bf16-format oracle, every step
 FP8_BAR = 0.05      # nats, fp8 cross memory vs the full-precision oracle, every step (max; measured 0.014)
 FP8_P99 = 0.02      # nats, its 99th percentile over all steps (measured 0.0087)
-# large-v3: every step of every STRIDE-th window of the batch goes through the oracle (the whole batch decodes on the
-# GPU either way); VLOG_AMD_RECORDS_STRIDE=1 sweeps every window (profiles/parity_r4_a_records_failure.jsonl)
+# large-v3: every step of every STRIDE-th window of the batch (windows OFFSET, OFFSET + STRIDE, ...) goes through the
+# oracle (the whole batch decodes on the GPU either way); VLOG_AMD_RECORDS_STRIDE=1 sweeps every window
+# (profiles/parity_r4_a_records_failure.jsonl)
 STRIDE = max(1, int(os.environ.get("VLOG_AMD_RECORDS_STRIDE", "4")))
+
+
+OFFSET = source_offset(STRIDE, "VLOG_AMD_RECORDS_OFFSET")
 
 
 def _record(name, **kw):
@@ -83,12 +87,13 @@ class RandomConfig:
         return self.enc[list(ws)].float().cpu().numpy()
 
 
-def sweep(cfg: RandomConfig, runs, chunk=8, stride=1):
+def sweep(cfg: RandomConfig, runs, chunk=8, stride=1, offset=0):
     """runs: {name: list of GenResult by window (None past its windows)}.  Every `stride`-th window's sequences of
-    every run teacher-forced through the oracle together (one cross-KV per window), per-step deviations per run."""
+    every run (from window `offset`) teacher-forced through the oracle together (one cross-KV per window), per-step
+    deviations per run."""
     names = list(runs)
     W = max(len(r) for r in runs.values())
-    sel = list(range(0, W, stride))
+    sel = list(range(offset % stride, W, stride))
     dev = {n: [] for n in names}
     ties = {n: 0 for n in names}
     worst = {n: (0.0, -1, -1) for n in names}
@@ -197,10 +202,10 @@ def test_config4_5_large_v3_greedy_beam_fp8_every_step(lv3):
     for r in beam:
         assert r.token_logprobs is not None and np.isfinite(r.token_logprobs).all()
         assert abs(float(np.sum(r.token_logprobs, dtype=np.float64)) - r.cum_logprob) < 1e-3 * max(1.0, abs(r.cum_logprob))
-    s = sweep(lv3, {"greedy": greedy, "fp8": fp8, "beam5": beam}, stride=STRIDE)
+    s = sweep(lv3, {"greedy": greedy, "fp8": fp8, "beam5": beam}, stride=STRIDE, offset=OFFSET)
     same_fp8 = sum(a.tokens == b.tokens for a, b in zip(greedy, fp8))
     _record(f"logprob records large-v3: greedy 150 / fp8 150 (vs full-precision oracle) / beam5 128, every step of "
-            f"every {STRIDE}th window", bar=BAR, fp8_bar=FP8_BAR, fp8_p99_bar=FP8_P99,
+            f"every {STRIDE}th window", bar=BAR, fp8_bar=FP8_BAR, fp8_p99_bar=FP8_P99, stride=STRIDE, offset=OFFSET,
             fp8_windows_identical_to_bf16=same_fp8, **s)
     assert s["greedy"]["max"] <= BAR and s["greedy"]["min_oracle_margin"] >= -BAR, s["greedy"]
     assert s["beam5"]["max"] <= BAR, s["beam5"]
