@@ -256,7 +256,7 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   512 rows; 0 disables).  Results agree to f32 rounding.
  *   "decode_gemm_big_lds" (default 72): LDS budget in KiB of the qkv / fc1 / fc2 ring blocks on that route, 72 (two
  *   resident blocks per CU) or 144 (one; the d x d projections always take 144).  Bit-identical either way.
- *   "decode_ln_fold" (default 1): passes of 33..1024 rows whose projections all take the ring route fold each
+ *   "decode_ln_fold" (default 0; measured slower, kept for A/B): passes of 33..1024 rows whose projections all take the ring route fold each
  *   pre-LayerNorm into its consumer: the residual producer writes bf16(x * gamma) and row sums, the consumer's
  *   epilogue applies rstd * acc - rstd * mean * (W gamma) + (W beta + bias), so no LayerNorm launch follows out and
  *   cout.  Results agree with 0 to the bf16 rounding of a different operand (not bit for bit).

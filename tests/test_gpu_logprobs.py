@@ -210,3 +210,19 @@ def test_config4_5_large_v3_greedy_beam_fp8_every_step(lv3):
     assert s["greedy"]["max"] <= BAR and s["greedy"]["min_oracle_margin"] >= -BAR, s["greedy"]
     assert s["beam5"]["max"] <= BAR, s["beam5"]
     assert s["fp8"]["max"] <= FP8_BAR and s["fp8"]["p99"] <= FP8_P99, s["fp8"]
+
+
+def test_large_v3_ln_fold_opt_in_every_step(lv3):
+    """The opt-in folded LayerNorm decode (decode_ln_fold=1: the residual producer writes bf16(x * gamma) and row
+    sums, the consumer GEMM's epilogue applies the LayerNorm; measured slower than the default, kept for A/B) on 48
+    large-v3 windows (ring passes): the same per-step bar against the oracle."""
+    lv3.eng.set_option("decode_ln_fold", 1)
+    try:
+        res = lv3.generate(W=48)
+    finally:
+        lv3.eng.set_option("decode_ln_fold", 0)
+    _self_consistent(res)
+    s = sweep(lv3, {"fold": res}, stride=STRIDE, offset=OFFSET)["fold"]
+    _record(f"logprob records large-v3 greedy 48 windows, decode_ln_fold=1, every {STRIDE}th window", bar=BAR,
+            stride=STRIDE, offset=OFFSET, **s)
+    assert s["max"] <= BAR and s["min_oracle_margin"] >= -BAR, s

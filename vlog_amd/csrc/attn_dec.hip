@@ -49,6 +49,10 @@ struct DecAttnArgs {
   // (zero between launches: the last arriver resets its word).
   const float* q_part; int q_splits, q_rows; const float* q_bias;
   int* cnt;
+  // self-attention of beam groups (sgroup = hypotheses per window > 1): the (row, head) pairs are walked as (window,
+  // head, hypothesis) in XCD-contiguous block order, so one head's waves of a window's beams run together on one XCD
+  // and the history rows the beams share (the lineage) are fetched from HBM once and served by its L1 / L2
+  int sgroup;
 };
 
 #define CT_MAX 1536
@@ -502,11 +506,22 @@ static void launch_group(int n_items, int cap, const DecAttnArgs& a, hipStream_t
 template <bool KSPLIT>
 __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int n_pairs) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int pair = KSPLIT ? (int)blockIdx.x : (int)blockIdx.x * 4 + wv;
+  const int H = a.H;
+  int pair, row, h;
+  if (a.sgroup > 1) {
+    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    pair = KSPLIT ? wgid : wgid * 4 + wv;
+    const int K = a.sgroup, j = pair % K, t = pair / K;
+    h = t % H;
+    row = (t / H) * K + j;
+  } else {
+    pair = KSPLIT ? (int)blockIdx.x : (int)blockIdx.x * 4 + wv;
+    row = pair / H;
+    h = pair - row * H;
+  }
   if (pair >= n_pairs) return;                         // KSPLIT: uniform over the block
   const int sub = lane & 7, g = lane >> 3;
-  const int H = a.H;
-  const int row = pair / H, h = pair - row * H;
   const int hyp = a.row_hyp[row];
   if (a.done && a.done[hyp]) return;
   const int nk = a.row_pos[row] + 1;
@@ -1104,10 +1119,11 @@ static void launch_k(bool self, dim3 grid, const DecAttnArgs& a, hipStream_t st,
 
 void launch_self_attn(const bf16* q, long long ldq, const bf16* kc, const bf16* vc, const int* lin, const int* row_hyp,
                       const int* row_pos, const int* done, bf16* out, long long ldo, int rows, int H, int n_ctx,
-                      unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, int plan_rows) {
+                      unsigned long long* stat, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, int plan_rows, int group) {
   if (rows <= 0) return;
   if (plan_rows < rows) plan_rows = rows;
   DecAttnArgs a{};
+  a.sgroup = group > 1 && rows % group == 0 ? group : 0;   // (the pair order only: results are the same either way)
   a.q = q; a.ldq = ldq; a.kbase = kc; a.vbase = vc; a.row_hyp = row_hyp; a.row_pos = row_pos; a.done = done; a.lin = lin;
   a.out = out; a.ldo = ldo; a.H = H; a.T = n_ctx; a.n_ctx = n_ctx; a.splits = 1;
   a.scale_log2 = 0.125f * 1.4426950408889634f; a.stat = stat;

@@ -38,7 +38,7 @@ void launch_im2col_conv1(const float*, long long, const int*, const int*, int, i
 void launch_zero_pad_rows(bf16*, int, long long, int, hipStream_t);
 void launch_attn_enc(const bf16*, bf16*, int, int, int, int, hipStream_t);
 void launch_self_attn(const bf16*, long long, const bf16*, const bf16*, const int*, const int*, const int*, const int*,
-                      bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t, int);
+                      bf16*, long long, int, int, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t, int, int);
 void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, const int*, const int*, const int*, bf16*,
                        long long, int, int, int, float*, float*, float*, float*, const int*, int, int, int,
                        const CrossFuse&, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
@@ -214,8 +214,10 @@ struct wm_engine {
   int dec_big128 = 0;        // ... from this many rows qkv / fc1 / fc2 in 128-row groups (0: never; VLOG_AMD_DEC_BIG128).
                              // Off: faster alone (dec_gemm_bench, 750 rows) but slower in the step (config 5, arms
                              // alternating on one box: dec_gemm 605 vs 566 ms per step, profiles/ab_r04_c5_big128.txt)
-  int dec_ln_fold = 1;       // ring passes (33..1024 rows): LayerNorms folded into their consumers (no combine launch
-                             // after out / cout; fc2's combine writes stats instead of the LayerNorm)
+  int dec_ln_fold = 0;       // ring passes (33..1024 rows): LayerNorms folded into their consumers (no combine launch
+                             // after out / cout; fc2's combine writes stats instead of the LayerNorm).  Off: the
+                             // consumers' epilogue costs more than the two launches it removes (dec_gemm 336 vs 319
+                             // ms per step at 150 rows, 656 vs 568 at 750; profiles/ab_r05_ln_fold_v2.txt)
   int dec_big_lds = 72;      // ... qkv / fc1 / fc2 with this LDS budget per ring block (KiB): 72 = two resident blocks
                              // per CU (tools/dec_gemm_bench at 750 rows: qkv 24.7 -> 18.8 us, fc1 31.3 -> 21.4, fc2
                              // 41.6 -> 33.1 against 144; at 256 rows qkv+fc1+fc2 45.6 -> 35.7 us per layer against the
@@ -676,7 +678,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
   {
     ProfScope ps(e, P_SELF_ATTN, st, 0, 0, true);
     launch_self_attn(q, d, kc, vc, lin, row_hyp, row_pos, done, ao, d, rows, H, C, e->dstat(P_SELF_ATTN), st, ps.a, ps.b,
-                     sl.total_rows);
+                     sl.total_rows, cross_group);
   }
   gemm(DEC_OUT, amat(ao, d), W.out_w, d, d, d,
        fold ? fold_producer(W.out_b, W.ln2_w) : ln_fuse ? resid_stat(W.out_b) : resid_ln(W.ln2_w, W.ln2_b, W.out_b));

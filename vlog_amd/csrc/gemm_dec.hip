@@ -185,7 +185,10 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
-template <int MF, int KIND, int R, int PK = 1, int NC = 1>
+// LNF: the folded-LayerNorm consumer (GemmA.fold_*): its row-sum loads are issued before the ring's first panels and
+// reduced after the last one (the epilogue is their only reader), in a separate instantiation so the plain kernel's
+// pipeline is untouched (a runtime-gated prologue made the compiler drain the DMA queue: 1.6x slower at 750 rows).
+template <int MF, int KIND, int R, int PK = 1, int NC = 1, bool LNF = false>
 __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
                                                        int K, GemmEpi epi, int tiles_n, int splitk, int kr,
                                                        float* __restrict__ part, int rgroups) {
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   constexpr int ROWS = MF * 16, HALF = MF / 2, WR = 32 * NC, SUB = (ROWS + WR) * 64, SLOT = PK * SUB, DA = ROWS / 32,
                 DPP = PK * (DA + NC);
   __shared__ __attribute__((aligned(16))) bf16 smem[R * SLOT];
-  __shared__ float sMR[2][ROWS];                        // folded LayerNorm: rstd and rstd * mean per row
+  __shared__ float sMR[2][LNF ? ROWS : 1];              // folded LayerNorm: rstd and rstd * mean per row
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -209,21 +212,25 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
   // folded LayerNorm (a.fold_stat): the row sums [M][tiles][2] of the block's rows are requested BEFORE the ring's
   // first panels and reduced after them, so their round trip overlaps the DMA latency; 8 threads per row, thread p
   // summing 16-B pairs of tiles p, p + 8, ... in order, then a fixed xor tree (every block forms the same bits)
-  constexpr int FCH = (ROWS + 31) / 32, FQ = 5;                  // 32-row chunks; up to 80 tiles = 40 pairs
-  f32x4 fq[FCH][FQ];
-  const bool fold = a.fold_stat != nullptr;
-  if (fold) {
+  constexpr int FCH = LNF ? (ROWS + 31) / 32 : 1, FT = LNF ? 10 : 1;  // 32-row chunks; up to 80 tiles = 8 x 10
+  // every load unconditional (clamped address, masked at the reduction): a select on a loaded value made the
+  // compiler wait for it (vmcnt(0)) before the ring's first DMAs
+  float2 fq[FCH][FT];
+  f32x4 pfs[LNF ? NC : 1], pfc[LNF ? NC : 1];
+  if constexpr (LNF) {
     const int T = a.fold_tiles, part = tid & 7;
 #pragma unroll
     for (int ch = 0; ch < FCH; ++ch) {
       const int gr = min(m0 + ch * 32 + (tid >> 3), M - 1);
       const float* sr = a.fold_stat + (long long)gr * T * 2;
 #pragma unroll
-      for (int j = 0; j < FQ; ++j) {
-        const int q = part + 8 * j;
-        if (T == 1) fq[ch][j] = (j == 0 && part == 0) ? f32x4{sr[0], sr[1], 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
-        else fq[ch][j] = 2 * q < T ? *(const f32x4*)(sr + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      for (int j = 0; j < FT; ++j) fq[ch][j] = *(const float2*)(sr + 2 * min(part + 8 * j, T - 1));
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col0 = min(n0 + (wc * NC + c) * 16 + 4 * (lane >> 4), N - 4);
+      pfs[c] = *(const f32x4*)(epi.fold_s + col0);
+      pfc[c] = *(const f32x4*)(epi.fold_c + col0);
     }
   }
   // DMA sources: wave `wid` moves A rows [wid*ROWS/4, +ROWS/4) (DA instructions of 8 rows) and W rows
@@ -268,31 +275,6 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
     for (int i = 0; i < HALF; ++i) acc[c][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int pre = min(R - 1, NP);
   for (int p = 0; p < pre; ++p) issue(p);
-  if (fold) {
-#pragma unroll
-    for (int ch = 0; ch < FCH; ++ch) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < FQ; ++j) {
-        s1 += fq[ch][j][0] + fq[ch][j][2];
-        s2 += fq[ch][j][1] + fq[ch][j][3];
-      }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        s1 += __shfl_xor(s1, o, 64);
-        s2 += __shfl_xor(s2, o, 64);
-      }
-      const int rr = ch * 32 + (tid >> 3);
-      if ((tid & 7) == 0 && rr < ROWS) {
-        const float mean = s1 / (float)K, var = fmaxf(s2 / (float)K - mean * mean, 0.f);
-        const float rs = rsqrtf(var + 1e-5f);
-        sMR[0][rr] = rs;
-        sMR[1][rr] = rs * mean;
-      }
-    }
-    // LDS only: the DMAs in flight are not waited for (a workgroup fence would drain vmcnt)
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
   for (int p = 0; p < NP; ++p) {
     vm_wait(min(NP - 1 - p, R - 2) * DPP);            // this wave's DMAs of super-panel p have landed
     asm volatile("s_barrier" ::: "memory");           // ... everyone's; slot of super-panel p-1 is free
@@ -324,6 +306,32 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
     }
   }
 
+  if constexpr (LNF) {
+    const int T = a.fold_tiles, part = tid & 7;
+#pragma unroll
+    for (int ch = 0; ch < FCH; ++ch) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < FT; ++j) {
+        const bool in = part + 8 * j < T;
+        s1 += in ? fq[ch][j].x : 0.f;
+        s2 += in ? fq[ch][j].y : 0.f;
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      const int rr = ch * 32 + (tid >> 3);
+      if ((tid & 7) == 0 && rr < ROWS) {
+        const float mean = s1 / (float)K, var = fmaxf(s2 / (float)K - mean * mean, 0.f);
+        const float rs = rsqrtf(var + 1e-5f);
+        sMR[0][rr] = rs;
+        sMR[1][rr] = rs * mean;
+      }
+    }
+    __syncthreads();
+  }
   const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -360,13 +368,12 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
       if (col0 >= N || row >= M) continue;
       if (to_slab) {
         *(f32x4*)(part + ((long long)split * M + row) * N + col0) = acc[c][i];
-      } else if (a.fold_stat) {
+      } else if (LNF) {
         // folded LayerNorm consumer: rstd (W . gx) - rstd mean (W g) + (W b + bias), then the epilogue kind
         const float rs = sMR[0][lr], rm = sMR[1][lr];
-        const f32x4 fs = *(const f32x4*)(epi.fold_s + col0), fc = *(const f32x4*)(epi.fold_c + col0);
         f32x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[c][i][e], rs, fc[e] - rm * fs[e]);
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[c][i][e], rs, pfc[c][e] - rm * pfs[c][e]);
         apply_epi4<KIND>(epi, row, col0, v);
       } else {
         apply_epi4<KIND>(epi, row, col0, acc[c][i]);
@@ -396,8 +403,8 @@ static int ring_lds_kb() {
   return v;
 }
 
-template <int MF, int KIND, int NC, int CAPKB>
-static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+template <int MF, int KIND, int NC, int CAPKB, bool LNF>
+static void run_ring_cap_f(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                          int splitk, int kr, hipStream_t st) {
   constexpr int SUBB = (MF * 16 + 32 * NC) * 128;      // bytes of one 64-k sub-panel
   constexpr int CAP = CAPKB * 1024;
@@ -409,7 +416,7 @@ static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, in
   const int pk = ring_pk();
   if constexpr (R4 >= 3) {
     if (pk == 4) {
-      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R4, 4, NC>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R4, 4, NC, LNF>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
                          splitk, kr, ws, rgroups);
       WM_LAUNCH_CHECK("dec_ring_kernel");
       return;
@@ -417,16 +424,28 @@ static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, in
   }
   if constexpr (R2 >= 3) {
     if (pk >= 2) {
-      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R2, 2, NC>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R2, 2, NC, LNF>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
                          splitk, kr, ws, rgroups);
       WM_LAUNCH_CHECK("dec_ring_kernel");
       return;
     }
   }
   static_assert(R * SUBB <= 160 * 1024, "ring exceeds the LDS");
-  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R, 1, NC>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk,
+  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R, 1, NC, LNF>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk,
                      kr, ws, rgroups);
   WM_LAUNCH_CHECK("dec_ring_kernel");
+}
+
+template <int MF, int KIND, int NC, int CAPKB>
+static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
+                         int splitk, int kr, hipStream_t st) {
+  if constexpr (KIND == EPI_BF16 || KIND == EPI_DEC_QKV) {
+    if (a.fold_stat) {
+      run_ring_cap_f<MF, KIND, NC, CAPKB, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+      return;
+    }
+  }
+  run_ring_cap_f<MF, KIND, NC, CAPKB, false>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
 }
 
 template <int MF, int KIND, int NC>
