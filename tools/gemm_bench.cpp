@@ -58,6 +58,9 @@ int main(int argc, char** argv) {
       {"square 4096", 4096, 4096, 4096, EPI_BF16},             // the guide's 8-phase template reference shape
       {"square 8192", 8192, 8192, 8192, EPI_BF16},
       {"enc.qkv K=4096", 24000, 3840, 4096, EPI_BF16},         // same tiles, 3.2x the K loop
+      {"enc.qkv (150 win)", 225000, 3840, 1280, EPI_BF16},     // the bench's encoder pass (150 windows)
+      {"enc.fc1 (150 win)", 225000, 5120, 1280, EPI_BF16},
+      {"enc.out (150 win)", 225000, 1280, 1280, EPI_RESID_F32},
   };
   size_t maxA = 0, maxW = 0, maxC = 0;
   for (auto& s : shapes) {
@@ -85,7 +88,9 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  const char* only = std::getenv("GEMM_ONLY");   // run only the shapes whose name contains this
   for (auto& s : shapes) {
+    if (only && !std::strstr(s.name, only)) continue;
     GemmEpi ep;
     std::memset(&ep, 0, sizeof(ep));
     ep.kind = s.kind;
