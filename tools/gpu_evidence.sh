@@ -23,11 +23,11 @@ echo "{\"cmd\": \"python3 bench.py --gpus 1 --steps 20 --warmup 5\", \"wall_s\":
 cat gpurun_out/bench_$TAG.json gpurun_out/bench_${TAG}_wall.json
 [ -n "$SKIP_PROF" ] && exit 0
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity > $R/gpurun_out/prof_$TAG.log 2>&1 || { tail -30 $R/gpurun_out/prof_$TAG.log; exit 1; }
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-variable > $R/gpurun_out/prof_$TAG.log 2>&1 || { tail -30 $R/gpurun_out/prof_$TAG.log; exit 1; }
 head -25 $(ls $R/gpurun_out/prof_$TAG/*kernel_stats.csv | head -1) | cut -d, -f1-5
 tail -1 $R/gpurun_out/prof_$TAG.log
 if [ -z "$NO_PMC" ]; then
-  bash $R/tools/pmc_traffic.sh || exit 1
+  BENCH_ARGS=--no-variable bash $R/tools/pmc_traffic.sh || exit 1
 fi
 [ -z "$WORKER" ] && exit 0
 cd $R
