@@ -260,6 +260,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   pre-LayerNorm into its consumer: the residual producer writes bf16(x * gamma) and row sums, the consumer's
  *   epilogue applies rstd * acc - rstd * mean * (W gamma) + (W beta + bias), so no LayerNorm launch follows out and
  *   cout.  Results agree with 0 to the bf16 rounding of a different operand (not bit for bit).
+ *   "align_fused" (default 1, process-wide): word alignment's z-score + median filter as one statistics kernel and
+ *   one wave-per-row-segment median kernel that recomputes z from the attention (never stored); 0 runs the two-kernel
+ *   form that writes z.  Bit-identical.
  *   "gemm_persistent" (default 0, process-wide): 1 runs large encoder GEMMs as one persistent block per CU
  *   walking its tiles, the next tile's first K-tiles loaded during the current tile's last K-steps and epilogue
  *   (measured no faster than one block per tile).  Bit-identical.

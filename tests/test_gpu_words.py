@@ -194,3 +194,34 @@ def test_large_v3_beam5_word_timestamps_128_windows():
         with open(p, "a") as f:
             f.write(json.dumps({"name": "large-v3 beam5+words 128 windows", "seconds": dt, "rtfx": W * 30.0 / dt,
                                 "segments": len(segs), "words": nw}) + "\n")
+
+
+@pytest.mark.parametrize("width", [7, 1, 3, 15])
+def test_fused_alignment_matrix_bit_identical(model, width):
+    """The fused z-score + median alignment kernels (option align_fused, default 1: f64 statistics, then one wave per
+    row segment recomputing z and taking the median from its neighbours' lanes) against the two-kernel form that
+    writes z: the same token probabilities and the same DTW path on every window, for ragged frame counts (the
+    reflect padding at both ends, a window shorter than one wave's segment) and every filter width class."""
+    eng, dims = model.engine, model.dims
+    W = 5
+    x = np.concatenate([speech_like(30.0, 700 + i) for i in range(W)])
+    feats = eng.features(torch.from_numpy(x))
+    enc = eng.encode(feats, [3000 * i for i in range(W)], [3000] * W)
+    eng.reserve(W, 8)
+    eng.cross_kv(enc, 0)
+    tok = Tokenizer(dims, language="en")
+    heads = dims.default_alignment_heads()
+    texts = [list(range(1200 + 5 * i, 1200 + 5 * i + n)) for i, n in enumerate((3, 40, 17, 1, 9))]
+    frames = [3000, 2402, 118, 60, 1999]
+    out = {}
+    try:
+        for fused in (0, 1):
+            eng.set_option("align_fused", fused)
+            assert eng.option("align_fused") == fused
+            out[fused] = eng.align_batch(list(range(W)), tok.sot_sequence, texts, frames, heads, width)
+    finally:
+        eng.set_option("align_fused", 1)
+    for w in range(W):
+        (p0, i0, j0), (p1, i1, j1) = out[0][w], out[1][w]
+        assert np.array_equal(p0, p1), w
+        assert np.array_equal(i0, i1) and np.array_equal(j0, j1), w

@@ -7,6 +7,7 @@
 //   dtw_kernel          : one workgroup per matrix, anti-diagonal wavefront over the (N+1) x (F+1) cost grid
 //                         (cells of one diagonal are independent), then a single-lane backtrace.
 #include "common.h"
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -108,6 +109,109 @@ __global__ __launch_bounds__(128) void align_median_kernel(const float* __restri
   mat[(long long)r * F + f] = -(acc / nh);
 }
 
+// Fused form of align_norm_kernel + align_median_kernel (the default since round 5): the z-score statistics
+// first (align_stats_kernel: per (head, frame) mean and 1/std over the token rows, f64, rows in order: the same
+// loop as align_norm_kernel's first pass), then one WAVE per (output row, 64 - 2 PAD frames) recomputes each z from
+// attn / rowsum with those statistics (the same f64 expression, so the same float) and takes the width-W median
+// from its neighbours' lanes (shuffles; the reflect padding maps to lanes the wave holds), summing the heads in
+// order.  z is never written: each attention value is read twice (statistics, median) instead of three times plus
+// a z write and its W-tap re-reads.  Bit-identical to the two-kernel form.
+__global__ __launch_bounds__(256) void align_stats_kernel(const float* __restrict__ attn, int S, int nh, int T, int F,
+                                                          const float* __restrict__ rowsum, double* __restrict__ stats) {
+  const int h = blockIdx.y;
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  double mean = 0.0, m2 = 0.0;
+  constexpr int U = 8;                                // rows in batches: loads first, then the sums in row order
+  for (int r0 = 0; r0 < S; r0 += U) {
+    float av[U], rs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = min(r0 + u, S - 1);
+      av[u] = attn[((long long)r * nh + h) * T + f];
+      rs[u] = rowsum[r * nh + h];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r0 + u >= S) break;
+      const double w = (double)av[u] / (double)rs[u];
+      mean += w;
+      m2 += w * w;
+    }
+  }
+  mean /= S;
+  const double var = fmax(m2 / S - mean * mean, 0.0);
+  stats[2 * ((long long)h * F + f)] = mean;
+  stats[2 * ((long long)h * F + f) + 1] = 1.0 / sqrt(var);
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(256) void align_zmed_kernel(const float* __restrict__ attn, int nh, int T, int F,
+                                                         const float* __restrict__ rowsum, const double* __restrict__ stats,
+                                                         int r0, int nrows, float* __restrict__ mat) {
+  constexpr int PAD = WIDTH / 2, OUT = 64 - 2 * PAD;   // output frames per wave
+  const int lane = threadIdx.x & 63;
+  const int nc = (F + OUT - 1) / OUT;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int r = gw / nc, c = gw - r * nc;
+  if (r >= nrows) return;                             // whole waves: the shuffles below see no exited lane
+  const int f0 = c * OUT;
+  const int ii = min(max(f0 - PAD + lane, 0), F - 1); // the frame whose z this lane computes
+  const int f = f0 + lane - PAD;                       // the frame this lane outputs (lanes PAD .. 63 - PAD)
+  int src[WIDTH];
+#pragma unroll
+  for (int k = 0; k < WIDTH; ++k) {
+    int i = f - PAD + k;
+    if (i < 0) i = -i;
+    if (i >= F) i = 2 * (F - 1) - i;
+    i = min(max(i, 0), F - 1);
+    src[k] = min(max(i - (f0 - PAD), 0), 63);
+  }
+  const int self = min(max(min(max(f, 0), F - 1) - (f0 - PAD), 0), 63);
+  const long long row = (long long)(r0 + r) * nh;
+  float acc = 0.f;
+  // heads in batches of U: every load of a batch issued before its first use (one memory round trip per batch,
+  // not per head); the heads are still summed one by one in order
+  constexpr int U = 8;
+  for (int h0 = 0; h0 < nh; h0 += U) {
+    float av[U], rs[U];
+    double mu[U], iv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int h = min(h0 + u, nh - 1);
+      av[u] = attn[(row + h) * T + ii];
+      rs[u] = rowsum[row + h];
+      mu[u] = stats[2 * ((long long)h * F + ii)];
+      iv[u] = stats[2 * ((long long)h * F + ii) + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    if (h0 + u >= nh) break;
+    const double w = (double)av[u] / (double)rs[u];
+    const float z = (float)((w - mu[u]) * iv[u]);
+    float v;
+    if (F <= PAD) {
+      v = __shfl(z, self, 64);
+    } else {
+      float t[WIDTH];
+#pragma unroll
+      for (int k = 0; k < WIDTH; ++k) t[k] = __shfl(z, src[k], 64);
+#pragma unroll
+      for (int round = 0; round < WIDTH; ++round)
+#pragma unroll
+        for (int k = round & 1; k + 1 < WIDTH; k += 2) {
+          const float lo = fminf(t[k], t[k + 1]), hi = fmaxf(t[k], t[k + 1]);
+          t[k] = lo;
+          t[k + 1] = hi;
+        }
+      v = t[PAD];
+    }
+    acc += v;
+    }
+  }
+  if (lane >= PAD && lane < 64 - PAD && f < F) mat[(long long)r * F + f] = -(acc / nh);
+}
+
 // cost [(N+1)][(M+1)] f32, trace [(N+1)][(M+1)] int8 scratch; x [N][M]; out path (text, time) reversed order fixed
 __device__ __forceinline__ void dtw_kernel_body(const float* __restrict__ x, int N, int M, float* __restrict__ cost,
                                                 signed char* __restrict__ trace, int* __restrict__ out_i,
@@ -169,11 +273,36 @@ void launch_token_probs(const float* logits, int rows, int V, int eot, const int
   WM_LAUNCH_CHECK("token_probs_kernel");
 }
 
+// Process-wide (wm_set_option "align_fused"; VLOG_AMD_ALIGN_FUSED): 0 runs the round-4 two-kernel form (A/B, tests)
+static int g_align_fused = [] {
+  const char* e = std::getenv("VLOG_AMD_ALIGN_FUSED");
+  return e ? std::atoi(e) : 1;
+}();
+static int align_fused() { return g_align_fused; }
+void align_set_fused(int on) { g_align_fused = on != 0; }
+int align_get_fused() { return g_align_fused; }
+
+// z: scratch of n_heads x S x F floats (the two-kernel form's z; the fused form keeps its f64 statistics there,
+// 4 floats per (head, frame): S >= 4 always holds for an aligned window, which has its sot prompt + text + eot)
 void launch_align_matrix(const float* attn, int S, int nh, int T, int F, int width, int r0, int nrows, float* rowsum,
                          float* z, float* mat, hipStream_t st) {
   if (width > MEDW_MAX || width % 2 != 1) throw std::runtime_error("median filter width must be odd and <= 15");
   hipLaunchKernelGGL(align_rowsum_kernel, dim3(S * nh), dim3(64), 0, st, attn, S, nh, T, F, rowsum);
   WM_LAUNCH_CHECK("align_rowsum_kernel");
+  if (align_fused() && S >= 4 && nrows > 0) {
+    double* stats = (double*)z;
+    hipLaunchKernelGGL(align_stats_kernel, dim3((F + 255) / 256, nh), dim3(256), 0, st, attn, S, nh, T, F, rowsum, stats);
+    WM_LAUNCH_CHECK("align_stats_kernel");
+    const int out = 64 - 2 * (width / 2), waves = nrows * ((F + out - 1) / out);
+    const dim3 g((waves + 3) / 4), b(256);
+    switch (width) {
+#define ZMED(W_) case W_: hipLaunchKernelGGL(align_zmed_kernel<W_>, g, b, 0, st, attn, nh, T, F, rowsum, stats, r0, nrows, mat); break;
+      ZMED(1) ZMED(3) ZMED(5) ZMED(7) ZMED(9) ZMED(11) ZMED(13) ZMED(15)
+#undef ZMED
+    }
+    WM_LAUNCH_CHECK("align_zmed_kernel");
+    return;
+  }
   hipLaunchKernelGGL(align_norm_kernel, dim3((F + 127) / 128, nh), dim3(128), 0, st, attn, S, nh, T, F, rowsum, z);
   WM_LAUNCH_CHECK("align_norm_kernel");
   const dim3 g((F + 127) / 128, nrows), b(128);

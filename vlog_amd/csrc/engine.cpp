@@ -57,6 +57,8 @@ void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, con
 
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
+void align_set_fused(int on);
+int align_get_fused();
 void launch_dtw(const float*, int, int, float*, signed char*, int*, int*, int*, hipStream_t);
 void launch_dtw_batch(const float*, const long long*, const int*, const int*, float*, signed char*, const long long*,
                       int*, int*, const long long*, int*, int, hipStream_t);
@@ -2584,6 +2586,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_attn_snake") e->xsnake = value != 0;
     else if (k == "cross_attn_keep") e->xkeep = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
     else if (k == "gemm_persistent") gemm_8p_set_persistent((int)value);
+    else if (k == "align_fused") align_set_fused((int)value);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
     else if (k == "cross_fp8") {
       // fp8 (OCP e4m3) cross memory in the factored form; switching re-allocates the window slots (their
@@ -2656,6 +2659,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_attn_snake") *value = e->xsnake;
     else if (k == "cross_attn_keep") *value = e->xkeep;
     else if (k == "gemm_persistent") *value = gemm_8p_get_persistent();
+    else if (k == "align_fused") *value = align_get_fused();
     else if (k == "encode_chunk") *value = e->enc_chunk;
     else if (k == "cross_fp8") *value = e->cross_fp8;
     else if (k == "cross_mode") *value = e->cross_mode;
