@@ -55,8 +55,16 @@ __global__ void align_norm_kernel(const float* __restrict__ attn, int S, int nh,
   }
 }
 
-__global__ void align_rowsum_kernel(const float* __restrict__ attn, int S, int nh, int T, int F, float* __restrict__ rowsum) {
+// blockIdx.y = window k of a batch (tS / tF: per-window rows and frames; null: one window of S rows, F frames);
+// window k's attention at attn + k astr, its row sums at rowsum + k rstr
+__global__ void align_rowsum_kernel(const float* __restrict__ attn, int S, int nh, int T, int F, float* __restrict__ rowsum,
+                                    const int* __restrict__ tS, const int* __restrict__ tF, long long astr, long long rstr) {
+  const int k = blockIdx.y;
+  if (tS) { S = tS[k]; F = tF[k]; }
   const int rh = blockIdx.x;     // r * nh + h
+  if (rh >= S * nh) return;
+  attn += k * astr;
+  rowsum += k * rstr;
   float s = 0.f;
   for (int f = threadIdx.x; f < F; f += 64) s += attn[(long long)rh * T + f];
   s = wave_sum(s);
@@ -117,10 +125,16 @@ __global__ __launch_bounds__(128) void align_median_kernel(const float* __restri
 // order.  z is never written: each attention value is read twice (statistics, median) instead of three times plus
 // a z write and its W-tap re-reads.  Bit-identical to the two-kernel form.
 __global__ __launch_bounds__(256) void align_stats_kernel(const float* __restrict__ attn, int S, int nh, int T, int F,
-                                                          const float* __restrict__ rowsum, double* __restrict__ stats) {
-  const int h = blockIdx.y;
+                                                          const float* __restrict__ rowsum, double* __restrict__ stats,
+                                                          const int* __restrict__ tS, const int* __restrict__ tF,
+                                                          long long astr, long long rstr, long long sstr) {
+  const int h = blockIdx.y, k = blockIdx.z;
+  if (tS) { S = tS[k]; F = tF[k]; }
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
+  attn += k * astr;
+  rowsum += k * rstr;
+  stats += k * sstr;
   double mean = 0.0, m2 = 0.0;
   constexpr int U = 8;                                // rows in batches: loads first, then the sums in row order
   for (int r0 = 0; r0 < S; r0 += U) {
@@ -148,9 +162,19 @@ __global__ __launch_bounds__(256) void align_stats_kernel(const float* __restric
 template <int WIDTH>
 __global__ __launch_bounds__(256) void align_zmed_kernel(const float* __restrict__ attn, int nh, int T, int F,
                                                          const float* __restrict__ rowsum, const double* __restrict__ stats,
-                                                         int r0, int nrows, float* __restrict__ mat) {
+                                                         int r0, int nrows, float* __restrict__ mat,
+                                                         const int* __restrict__ tF, const int* __restrict__ trows,
+                                                         const long long* __restrict__ tmat, long long astr, long long rstr,
+                                                         long long sstr) {
   constexpr int PAD = WIDTH / 2, OUT = 64 - 2 * PAD;   // output frames per wave
   const int lane = threadIdx.x & 63;
+  {
+    const int k = blockIdx.y;                          // window k of a batch (tables; null: one window)
+    if (tF) { F = tF[k]; nrows = trows[k]; mat += tmat[k]; }
+    attn += k * astr;
+    rowsum += k * rstr;
+    stats += k * sstr;
+  }
   const int nc = (F + OUT - 1) / OUT;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int r = gw / nc, c = gw - r * nc;
@@ -287,16 +311,18 @@ int align_get_fused() { return g_align_fused; }
 void launch_align_matrix(const float* attn, int S, int nh, int T, int F, int width, int r0, int nrows, float* rowsum,
                          float* z, float* mat, hipStream_t st) {
   if (width > MEDW_MAX || width % 2 != 1) throw std::runtime_error("median filter width must be odd and <= 15");
-  hipLaunchKernelGGL(align_rowsum_kernel, dim3(S * nh), dim3(64), 0, st, attn, S, nh, T, F, rowsum);
+  hipLaunchKernelGGL(align_rowsum_kernel, dim3(S * nh), dim3(64), 0, st, attn, S, nh, T, F, rowsum, nullptr, nullptr, 0LL, 0LL);
   WM_LAUNCH_CHECK("align_rowsum_kernel");
   if (align_fused() && S >= 4 && nrows > 0) {
     double* stats = (double*)z;
-    hipLaunchKernelGGL(align_stats_kernel, dim3((F + 255) / 256, nh), dim3(256), 0, st, attn, S, nh, T, F, rowsum, stats);
+    hipLaunchKernelGGL(align_stats_kernel, dim3((F + 255) / 256, nh, 1), dim3(256), 0, st, attn, S, nh, T, F, rowsum, stats,
+                       nullptr, nullptr, 0LL, 0LL, 0LL);
     WM_LAUNCH_CHECK("align_stats_kernel");
     const int out = 64 - 2 * (width / 2), waves = nrows * ((F + out - 1) / out);
     const dim3 g((waves + 3) / 4), b(256);
     switch (width) {
-#define ZMED(W_) case W_: hipLaunchKernelGGL(align_zmed_kernel<W_>, g, b, 0, st, attn, nh, T, F, rowsum, stats, r0, nrows, mat); break;
+#define ZMED(W_) case W_: hipLaunchKernelGGL(align_zmed_kernel<W_>, g, b, 0, st, attn, nh, T, F, rowsum, stats, r0, nrows, mat, \
+                                             nullptr, nullptr, nullptr, 0LL, 0LL, 0LL); break;
       ZMED(1) ZMED(3) ZMED(5) ZMED(7) ZMED(9) ZMED(11) ZMED(13) ZMED(15)
 #undef ZMED
     }
@@ -312,6 +338,33 @@ void launch_align_matrix(const float* attn, int S, int nh, int T, int F, int wid
 #undef MEDW
   }
   WM_LAUNCH_CHECK("align_median_kernel");
+}
+
+// Every window of an alignment chunk at once (the fused form): window k's attention at attn + k smax nh T
+// ([S_k][nh][T]), rows S_k (tS), frames F_k (tF), output rows rows_k (trows) written at mat + tmat[k]; scratch:
+// rowsum [c][smax][nh] f32, stats [c][nh][fmax][2] f64.  One launch per kernel for the chunk instead of three per
+// window (each window's launch alone was ~1.5 workgroups per CU: the median's head loop ran latency-bound).
+void launch_align_matrix_batch(const float* attn, int c, int smax, int nh, int T, int fmax, int rows_max, int width,
+                               int r0, const int* tS, const int* tF, const int* trows, const long long* tmat,
+                               float* rowsum, double* stats, float* mat, hipStream_t st) {
+  if (width > MEDW_MAX || width % 2 != 1) throw std::runtime_error("median filter width must be odd and <= 15");
+  if (c <= 0) return;
+  const long long astr = (long long)smax * nh * T, rstr = (long long)smax * nh, sstr = 2LL * nh * fmax;
+  hipLaunchKernelGGL(align_rowsum_kernel, dim3(smax * nh, c), dim3(64), 0, st, attn, smax, nh, T, fmax, rowsum, tS, tF,
+                     astr, rstr);
+  WM_LAUNCH_CHECK("align_rowsum_kernel");
+  hipLaunchKernelGGL(align_stats_kernel, dim3((fmax + 255) / 256, nh, c), dim3(256), 0, st, attn, smax, nh, T, fmax, rowsum,
+                     stats, tS, tF, astr, rstr, sstr);
+  WM_LAUNCH_CHECK("align_stats_kernel");
+  const int out = 64 - 2 * (width / 2), waves = rows_max * ((fmax + out - 1) / out);
+  const dim3 g((waves + 3) / 4, c), b(256);
+  switch (width) {
+#define ZMED(W_) case W_: hipLaunchKernelGGL(align_zmed_kernel<W_>, g, b, 0, st, attn, nh, T, fmax, rowsum, stats, r0, \
+                                           rows_max, mat, tF, trows, tmat, astr, rstr, sstr); break;
+    ZMED(1) ZMED(3) ZMED(5) ZMED(7) ZMED(9) ZMED(11) ZMED(13) ZMED(15)
+#undef ZMED
+  }
+  WM_LAUNCH_CHECK("align_zmed_kernel");
 }
 
 void launch_dtw(const float* x, int N, int M, float* cost, signed char* trace, int* out_i, int* out_j, int* out_len,

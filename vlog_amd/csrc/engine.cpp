@@ -57,6 +57,8 @@ void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, con
 
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
+void launch_align_matrix_batch(const float*, int, int, int, int, int, int, int, int, const int*, const int*, const int*,
+                               const long long*, float*, double*, float*, hipStream_t);
 void align_set_fused(int on);
 int align_get_fused();
 void launch_dtw(const float*, int, int, float*, signed char*, int*, int*, int*, hipStream_t);
@@ -2106,7 +2108,10 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
     while (i1 < n) {
       const int it = ord[i1];
       const int s2 = std::max(smax, S[it]);
-      const double bytes = (double)(i1 - i0 + 1) * (s2 * n_heads * T * 4 + per_item_kv) + (double)(ntext + nt[it]) * V * 4;
+      // per item: its attention capture, the factored form's K/V gather, and the fused alignment's f64 statistics
+      // (n_heads x F x 2 doubles, F <= T / 2)
+      const double bytes = (double)(i1 - i0 + 1) * (s2 * n_heads * T * 4 + per_item_kv + (double)n_heads * T * 8) +
+                           (double)(ntext + nt[it]) * V * 4;
       if (i1 > i0 && (bytes > budget || (double)(i1 - i0 + 1) * s2 > 1.25 * (double)(sum_s + S[it]))) break;
       smax = s2;
       ntext += nt[it];
@@ -2148,30 +2153,47 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
       pt += Ns[k] + Ms[k];
     }
     e->a_mat.ensure((size_t)xt * 4);
-    e->a_rowsum.ensure((size_t)smax * n_heads * 4);
-    e->a_z.ensure((size_t)n_heads * smax * T * 4);
-    for (int k = 0; k < c; ++k) {
-      const int i = ord[i0 + k];
-      launch_align_matrix(e->a_attn.as<float>() + (size_t)k * smax * n_heads * T, S[i], n_heads, T, F[i], medw, sot_len,
-                          nt[i] + 1, e->a_rowsum.as<float>(), e->a_z.as<float>(), e->a_mat.as<float>() + xo[k], st);
-    }
-    e->a_cost.ensure((size_t)ct * 4);
-    e->a_trace.ensure((size_t)ct);
-    e->a_pi.ensure((size_t)pt * 4);
-    e->a_pj.ensure((size_t)pt * 4);
-    e->a_plen.ensure((size_t)c * 4);
-    e->a_meta.ensure((size_t)c * (3 * 8 + 2 * 4));
+    e->a_meta.ensure((size_t)c * (3 * 8 + 3 * 4));
     char* meta = (char*)e->a_meta.p;
     long long* d_xo = (long long*)meta;
     long long* d_co = d_xo + c;
     long long* d_po = d_co + c;
     int* d_N = (int*)(d_po + c);
     int* d_M = d_N + c;
+    int* d_S = d_M + c;
+    std::vector<int> Ss(c);
+    int fmax = 0, nmax = 0;
+    for (int k = 0; k < c; ++k) {
+      Ss[k] = S[ord[i0 + k]];
+      fmax = std::max(fmax, Ms[k]);
+      nmax = std::max(nmax, Ns[k]);
+    }
     HIP_OK(hipMemcpyAsync(d_xo, xo.data(), c * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_co, co.data(), c * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_po, po.data(), c * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_N, Ns.data(), c * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_M, Ms.data(), c * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_S, Ss.data(), c * 4, hipMemcpyHostToDevice, st));
+    if (align_get_fused()) {
+      // the whole chunk in three launches (rows of window k: its text + <|endoftext|>, from row sot_len)
+      e->a_rowsum.ensure((size_t)c * smax * n_heads * 4);
+      e->a_z.ensure((size_t)c * n_heads * fmax * 16);
+      launch_align_matrix_batch(e->a_attn.as<float>(), c, smax, n_heads, T, fmax, nmax, medw, sot_len, d_S, d_M, d_N, d_xo,
+                                e->a_rowsum.as<float>(), (double*)e->a_z.p, e->a_mat.as<float>(), st);
+    } else {
+      e->a_rowsum.ensure((size_t)smax * n_heads * 4);
+      e->a_z.ensure((size_t)n_heads * smax * T * 4);
+      for (int k = 0; k < c; ++k) {
+        const int i = ord[i0 + k];
+        launch_align_matrix(e->a_attn.as<float>() + (size_t)k * smax * n_heads * T, S[i], n_heads, T, F[i], medw, sot_len,
+                            nt[i] + 1, e->a_rowsum.as<float>(), e->a_z.as<float>(), e->a_mat.as<float>() + xo[k], st);
+      }
+    }
+    e->a_cost.ensure((size_t)ct * 4);
+    e->a_trace.ensure((size_t)ct);
+    e->a_pi.ensure((size_t)pt * 4);
+    e->a_pj.ensure((size_t)pt * 4);
+    e->a_plen.ensure((size_t)c * 4);
     launch_dtw_batch(e->a_mat.as<float>(), d_xo, d_N, d_M, e->a_cost.as<float>(), e->a_trace.as<signed char>(), d_co,
                      e->a_pi.as<int>(), e->a_pj.as<int>(), d_po, e->a_plen.as<int>(), c, st);
     std::vector<int> pi(pt), pj(pt), plen(c);
