@@ -312,7 +312,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   }
   // one tile: its staged registers -> the wave's LDS image, the loads of the next tile into the same
   // registers, then S^T, the cross-wave sum, the online softmax and U^T
-  auto tile_step = [&](int tile, auto& stg, float& scl) {
+  auto tile_step = [&](int tile, auto& stg, float& scl, int ahead) {
     int lo = lane;
     asm volatile("" : "+v"(lo));
     bf16* sEA = sE;                                       // rows 0-15 of this tile
@@ -345,7 +345,7 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
       }
     }
     if (F8 && lo < 32) sScale[lo] = scl;
-    if (tile + 1 < te) load(stg, scl, tile + 1, lo);
+    if (tile + ahead < te) load(stg, scl, tile + ahead, lo);
     // ---- S^T partial over this wave's columns
     f32x16 sc = xzero16();
     {
@@ -454,8 +454,21 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
         }
     }
   };
-  if (tb < te) load(stgA, scA, tb, lane);
-  for (int tile = tb; tile < te; ++tile) tile_step(tile, stgA, scA);
+  if constexpr ((ABL & 32) != 0) {
+    // microbenchmark only (bit 5): two register staging sets, each tile's loads issued two tiles ahead -- does
+    // the load path stream faster with twice the bytes in flight per wave?  (Loads-only: ABL 39.)
+    i32x4 stgB[LS];
+    float scB = 1.f;
+    if (tb < te) load(stgA, scA, tb, lane);
+    if (tb + 1 < te) load(stgB, scB, tb + 1, lane);
+    for (int tile = tb; tile < te; tile += 2) {
+      tile_step(tile, stgA, scA, 2);
+      if (tile + 1 < te) tile_step(tile + 1, stgB, scB, 2);
+    }
+  } else {
+    if (tb < te) load(stgA, scA, tb, lane);
+    for (int tile = tb; tile < te; ++tile) tile_step(tile, stgA, scA, 1);
+  }
   l_run += __shfl_xor(l_run, 32, 64);
   if (valid) {
     const float inv = 1.0f / l_run;
@@ -814,10 +827,10 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
     case AB_: hipLaunchKernelGGL((xattn_kernel<160, 8, 1, F8_, AB_>), grid, dim3(512), 0, st, a); break;
     if (escale) {
       switch (a.abl) { XA_ABL(true, 1) XA_ABL(true, 2) XA_ABL(true, 4) XA_ABL(true, 7) XA_ABL(true, 8) XA_ABL(true, 16)
-                       XA_ABL(true, 23) default: throw std::runtime_error("xattn: unsupported ablation"); }
+                       XA_ABL(true, 23) XA_ABL(true, 39) default: throw std::runtime_error("xattn: unsupported ablation"); }
     } else {
       switch (a.abl) { XA_ABL(false, 1) XA_ABL(false, 2) XA_ABL(false, 4) XA_ABL(false, 7) XA_ABL(false, 8)
-                       XA_ABL(false, 16) XA_ABL(false, 23) default: throw std::runtime_error("xattn: unsupported ablation"); }
+                       XA_ABL(false, 16) XA_ABL(false, 23) XA_ABL(false, 39) default: throw std::runtime_error("xattn: unsupported ablation"); }
     }
 #undef XA_ABL
     WM_LAUNCH_CHECK("xattn_kernel");
