@@ -109,6 +109,25 @@ class _HFVocab:
         return self.tok.token_to_id(s)
 
 
+# Vocabularies are immutable once built and cost a model's worth of work to build (the synthetic one: 0.3 s of
+# seeded word generation; a tokenizer.json: a file parse), while faster-whisper builds a Tokenizer per transcribe
+# call around a tokenizer it loaded once.  So they are built once per process and shared.
+_VOCABS: Dict[tuple, object] = {}
+
+
+def _vocab_for(st: SpecialTokens, n_vocab: int, tokenizer_json: Optional[str], seed: int):
+    if tokenizer_json and os.path.isfile(tokenizer_json):
+        path = os.path.abspath(tokenizer_json)
+        key = ("json", path, os.path.getmtime(path))
+        if key not in _VOCABS:
+            _VOCABS[key] = _HFVocab(path)
+    else:
+        key = ("synthetic", n_vocab, st.eot, st.sot, st.lang_begin, st.timestamp_begin, seed)
+        if key not in _VOCABS:
+            _VOCABS[key] = _SyntheticVocab(st, n_vocab, seed)
+    return _VOCABS[key]
+
+
 class Tokenizer:
     """faster-whisper-shaped tokenizer: Tokenizer(vocab, multilingual, task, language)."""
 
@@ -117,13 +136,11 @@ class Tokenizer:
         self.dims = dims
         self.st = dims.specials
         self.multilingual = dims.multilingual
-        if tokenizer_json and os.path.isfile(tokenizer_json):
-            self.vocab = _HFVocab(tokenizer_json)
+        self.vocab = _vocab_for(self.st, dims.n_vocab, tokenizer_json, seed)
+        if isinstance(self.vocab, _HFVocab):
             sot = self.vocab.token_to_id("<|startoftranscript|>")
             if sot is not None and sot != self.st.sot:
                 raise ValueError(f"tokenizer.json <|startoftranscript|>={sot} does not match the model layout")
-        else:
-            self.vocab = _SyntheticVocab(self.st, dims.n_vocab, seed)
         self.task = self.transcribe if task == "transcribe" else self.translate if task == "translate" else None
         self.language_code = language or "en"
         self.language = self.st.lang_token(self.language_code) if (self.multilingual and language) else None
