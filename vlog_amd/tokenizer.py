@@ -213,6 +213,15 @@ class Tokenizer:
             return self.split_tokens_on_unicode(tokens)
         return self.split_tokens_on_spaces(tokens)
 
+    def _decode_one(self, t: int) -> str:
+        """decode_with_timestamps([t]), memoised on the (shared, immutable) vocabulary: word splitting decodes most
+        tokens alone, once per word."""
+        memo = self.vocab.__dict__.setdefault("_one", {})
+        s = memo.get(t)
+        if s is None:
+            s = memo[t] = self.decode_with_timestamps([t])
+        return s
+
     def split_tokens_on_unicode(self, tokens: List[int]):
         full = self.decode_with_timestamps(tokens)
         rep = "�"
@@ -220,7 +229,7 @@ class Tokenizer:
         off = 0
         for t in tokens:
             cur.append(t)
-            dec = self.decode_with_timestamps(cur)
+            dec = self._decode_one(int(t)) if len(cur) == 1 else self.decode_with_timestamps(cur)
             idx = dec.find(rep)
             idx = None if idx < 0 else idx + off
             if idx is None or (idx < len(full) and full[idx] == rep):
