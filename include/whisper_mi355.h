@@ -145,7 +145,7 @@ typedef struct wm_generate_args {
    * when one ends, its row takes the next window in h_slots order at the next host check (the new window's prompt
    * is prefilled inside that step's decoder pass), so the step count follows the total work instead of the longest
    * window.  Order the windows longest-expected first (vlog_amd/shard.py expected_tokens).  compact = 1: once no
-   * window is waiting, finished rows are dropped from the passes when the live rows fall to 5/8 of the pass (the
+   * window is waiting, finished rows are dropped from the passes when the live rows fall to 7/8 of the pass (the
    * step graph is re-captured for the new row count).  Each window's result is the same computation either way;
    * the GEMM / attention routes follow the pass's row count, so results agree to f32 rounding, not bit for bit.
    * Beam search: max_rows (a multiple of beam_size is used: max_rows / beam_size windows in flight) refills a

@@ -88,6 +88,20 @@ thread_local std::string g_err;
 // PER ENGINE: `guarded` points t_realloc at the engine whose entry point runs on this thread (under its lock), so
 // another engine's allocations neither force a re-capture nor fail a capture in progress.  Allocations outside an
 // entry point (wm_create) count on a fallback no graph reads.
+// Greedy row-set compaction threshold in eighths of the pass (VLOG_AMD_COMPACT_8THS, default 7): the live rows are
+// packed once they fall to this many eighths of the pass's rows (a step-graph re-capture per compaction).  Variable
+// workload, arms alternating on one box: 4/8 2605, 5/8 2644-2645, 6/8 2660-2672, 7/8 2680 RTFx, the same tokens
+// (profiles/ab_r05_compact.txt): the cross-attention's items track the live windows more closely, and a re-capture
+// costs less than the passes over finished rows it saves.
+static int row_compact_8ths() {
+  static const int v = [] {
+    const char* e = std::getenv("VLOG_AMD_COMPACT_8THS");
+    const int x = e ? std::atoi(e) : 7;
+    return x >= 1 && x <= 7 ? x : 7;
+  }();
+  return v;
+}
+
 thread_local long long* t_realloc = nullptr;
 long long g_realloc_none = 0;
 inline long long& realloc_gen() { return t_realloc ? *t_realloc : g_realloc_none; }
@@ -1187,7 +1201,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
     HIP_OK(hipStreamWaitEvent(e->gst, e->ev_g0, 0));
     ds = e->gst;
   }
-  // Beam compaction (a->compact): once the live windows' hypotheses fill <= 5/8 of the pass, the pass keeps only
+  // Beam compaction (a->compact): once the live windows' hypotheses fill <= 7/8 of the pass, the pass keeps only
   // them (row r -> hypothesis row_hyp[r], window groups stay contiguous); the beam state stays where it is, per
   // hypothesis (KV cache, lineage, tokens), so the rows' tokens / positions are gathered per pass (rows_fill) and
   // the selection reads its logits row by row.  Finished windows then stop costing GEMM rows in the tail.
@@ -1379,7 +1393,7 @@ void generate(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
 // row per live hypothesis + P prompt rows per new one; the final LayerNorm gathers one logits row per row-set row
 // in row order), so a refill costs no extra pass.  Rows stay in place while windows wait, so the captured step
 // graph stays valid; once the queue is empty and compaction is on, the live rows are packed densely when they
-// fall to 5/8 of the pass (re-capture for the new count).  A finished hypothesis' tokens are copied to the
+// fall to 7/8 of the pass (row_compact_8ths; re-capture for the new count).  A finished hypothesis' tokens are copied to the
 // per-window output tables by the block that ends it (search.hip), since its slot is then reused.
 void generate_rows(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   const auto& m = e->dm;
@@ -1556,7 +1570,7 @@ void generate_rows(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
         n_free = nrows - n_live;
         if (n_live == 0 && next >= W) break;
         const bool refill = next < W && (n_free >= refill_min || n_live == 0);
-        const bool compact = next >= W && a->compact && n_live * 8 <= nrows * 5;
+        const bool compact = next >= W && a->compact && n_live * 8 <= nrows * row_compact_8ths();
         if (refill || compact) {
           carry.clear(); new_row_hyp.clear(); starts.clear();
           for (int r = 0; r < nrows; ++r) {
