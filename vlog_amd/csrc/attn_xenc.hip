@@ -771,7 +771,7 @@ void launch_xq(const bf16* q, long long ldq, const CrossFuse& fz, const bf16* wk
 }
 
 // Key splits of a pass.  A function of the whole pass, so slicing a pass into launches never changes a
-// row's arithmetic: about 1.75 rounds of 256 one-workgroup CUs (measured on the 150-window large-v3
+// row's arithmetic: about 1.75 rounds of 256 one-workgroup CUs (at most 8) (measured on the 150-window large-v3
 // decode: 1 / 2 / 3 / 4 / 5 splits -> 522 / 564 / 450 / 510 / 483 ms of attention per bench step; fewer,
 // longer items amortise each item's prologue and epilogue, more of them fill the last round), at most 16,
 // at least one 32-position tile per split, and the bf16 partial slabs capped at 256 MB.
@@ -780,13 +780,22 @@ int xattn_splits(int plan_rows, int group, int H, int T, int d) {
     const char* e = std::getenv("VLOG_AMD_XSPLITS");
     return e ? std::atoi(e) : 0;
   }();
+  // At most 8 splits: the split merge (xcomb) takes 9-16 splits in 10 dependent load batches (5 for 5-8), and the
+  // row set's small tail passes (16 splits by the rule below) paid more there than the attention gained (variable
+  // workload: 2657-2680 RTFx uncapped, 2698-2711 capped at 4-8, profiles/ab_r05_xsplits_max.txt).
+  // VLOG_AMD_XSPLITS_MAX overrides the cap (A/B).
+  static const int cap_env = [] {
+    const char* e = std::getenv("VLOG_AMD_XSPLITS_MAX");
+    return e ? std::max(0, std::atoi(e)) : 0;    // 0: the rule
+  }();
+  const int cap = cap_env > 0 ? cap_env : 8;
   const int groups = std::max(1, plan_rows / std::max(group, 1));
   const long long n_mt = ((long long)group * H + 31) / 32;
   const long long items = groups * n_mt;
   const int n_tiles = (T + 31) / 32;
   int s = (int)((448 + items / 2) / items);
   if (forced > 0) s = forced;
-  s = std::max(1, std::min(s, std::min(XMAXS, n_tiles)));
+  s = std::max(1, std::min(s, std::min(std::min(cap, XMAXS), n_tiles)));
   const long long slab = (long long)plan_rows * H * d * 2;
   while (s > 1 && slab * s > (256LL << 20)) --s;
   return s;
