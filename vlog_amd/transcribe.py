@@ -541,7 +541,7 @@ class WhisperModel:
             jump_times = time_idx[jumps] / self.tokens_per_second
             starts = jump_times[wb[:-1]]
             ends = jump_times[wb[1:]]
-            wprob = [float(np.mean(probs[i:j])) for i, j in zip(wb[:-1], wb[1:])]
+            wprob = _word_means(probs, wb)
             out.append([dict(word=w, tokens=t, start=float(s), end=float(e), probability=p)
                         for w, t, s, e, p in zip(words, word_tokens, starts, ends, wprob)])
         return out
@@ -614,6 +614,19 @@ class WhisperModel:
 def _get_end(segments: List[dict]) -> Optional[float]:
     return next((w["end"] for s in reversed(segments) for w in reversed(s.get("words") or [])),
                 segments[-1]["end"] if segments else None)
+
+
+def _word_means(probs: np.ndarray, wb: np.ndarray) -> List[float]:
+    """[float(np.mean(probs[i:j])) ...] over consecutive word boundaries, with np.mean's own arithmetic spelled out for
+    float32 (np.add.reduce of the slice, divided by the count in float64, rounded to float32): the same values
+    without np.mean's per-call overhead (half the host time of config 5's word probabilities)."""
+    p = np.asarray(probs)
+    b = np.asarray(wb).tolist()
+    if p.dtype != np.float32:
+        return [float(np.mean(p[i:j])) for i, j in zip(b[:-1], b[1:])]
+    add = np.add.reduce
+    return [float(np.float32(float(add(p[i:j])) / (j - i))) if j > i else float(np.mean(p[i:j]))
+            for i, j in zip(b[:-1], b[1:])]
 
 
 def merge_punctuations(alignment: List[dict], prepended: str, appended: str) -> None:
