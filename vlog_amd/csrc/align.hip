@@ -7,6 +7,7 @@
 //   dtw_kernel          : one workgroup per matrix, anti-diagonal wavefront over the (N+1) x (F+1) cost grid
 //                         (cells of one diagonal are independent), then a single-lane backtrace.
 #include "common.h"
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -350,21 +351,28 @@ void launch_align_matrix_batch(const float* attn, int c, int smax, int nh, int T
   if (width > MEDW_MAX || width % 2 != 1) throw std::runtime_error("median filter width must be odd and <= 15");
   if (c <= 0) return;
   const long long astr = (long long)smax * nh * T, rstr = (long long)smax * nh, sstr = 2LL * nh * fmax;
-  hipLaunchKernelGGL(align_rowsum_kernel, dim3(smax * nh, c), dim3(64), 0, st, attn, smax, nh, T, fmax, rowsum, tS, tF,
-                     astr, rstr);
-  WM_LAUNCH_CHECK("align_rowsum_kernel");
-  hipLaunchKernelGGL(align_stats_kernel, dim3((fmax + 255) / 256, nh, c), dim3(256), 0, st, attn, smax, nh, T, fmax, rowsum,
-                     stats, tS, tF, astr, rstr, sstr);
-  WM_LAUNCH_CHECK("align_stats_kernel");
-  const int out = 64 - 2 * (width / 2), waves = rows_max * ((fmax + out - 1) / out);
-  const dim3 g((waves + 3) / 4, c), b(256);
-  switch (width) {
-#define ZMED(W_) case W_: hipLaunchKernelGGL(align_zmed_kernel<W_>, g, b, 0, st, attn, nh, T, fmax, rowsum, stats, r0, \
-                                           rows_max, mat, tF, trows, tmat, astr, rstr, sstr); break;
-    ZMED(1) ZMED(3) ZMED(5) ZMED(7) ZMED(9) ZMED(11) ZMED(13) ZMED(15)
+  // windows on grid.y / grid.z: at most 65535 per launch
+  for (int k0 = 0; k0 < c; k0 += 65535) {
+    const int cc = std::min(c - k0, 65535);
+    const float* at = attn + k0 * astr;
+    float* rs = rowsum + k0 * rstr;
+    double* sts = stats + k0 * sstr;
+    hipLaunchKernelGGL(align_rowsum_kernel, dim3(smax * nh, cc), dim3(64), 0, st, at, smax, nh, T, fmax, rs, tS + k0,
+                       tF + k0, astr, rstr);
+    WM_LAUNCH_CHECK("align_rowsum_kernel");
+    hipLaunchKernelGGL(align_stats_kernel, dim3((fmax + 255) / 256, nh, cc), dim3(256), 0, st, at, smax, nh, T, fmax, rs,
+                       sts, tS + k0, tF + k0, astr, rstr, sstr);
+    WM_LAUNCH_CHECK("align_stats_kernel");
+    const int out = 64 - 2 * (width / 2), waves = rows_max * ((fmax + out - 1) / out);
+    const dim3 g((waves + 3) / 4, cc), b(256);
+    switch (width) {
+#define ZMED(W_) case W_: hipLaunchKernelGGL(align_zmed_kernel<W_>, g, b, 0, st, at, nh, T, fmax, rs, sts, r0, rows_max, \
+                                             mat, tF + k0, trows + k0, tmat + k0, astr, rstr, sstr); break;
+      ZMED(1) ZMED(3) ZMED(5) ZMED(7) ZMED(9) ZMED(11) ZMED(13) ZMED(15)
 #undef ZMED
+    }
+    WM_LAUNCH_CHECK("align_zmed_kernel");
   }
-  WM_LAUNCH_CHECK("align_zmed_kernel");
 }
 
 void launch_dtw(const float* x, int N, int M, float* cost, signed char* trace, int* out_i, int* out_j, int* out_len,
