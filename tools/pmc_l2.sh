@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 mkdir -p $R/gpurun_out/pmc_l2
 timeout -s KILL 300 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KREGEX" \
   --output-format csv -d $R/gpurun_out/pmc_l2/run -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-profile \
-  --no-cpu-baseline --no-parity > $R/gpurun_out/pmc_l2/run.log 2>&1 || { tail -20 $R/gpurun_out/pmc_l2/run.log; exit 1; }
+  --no-cpu-baseline --no-parity --no-variable > $R/gpurun_out/pmc_l2/run.log 2>&1 || { tail -20 $R/gpurun_out/pmc_l2/run.log; exit 1; }
 python3 - "$R/gpurun_out/pmc_l2" <<'PY'
 import csv, glob, json, os, sys
 from collections import defaultdict
