@@ -522,18 +522,18 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
   }
   if (pair >= n_pairs) return;                         // KSPLIT: uniform over the block
   const int sub = lane & 7, g = lane >> 3;
+  // the row's hypothesis, position and q go out together; the done flag (a second dependent load) is only read at
+  // the store, so a live row's K/V requests no longer wait for it (a finished row's loads stay in bounds: its
+  // position is clamped to the context and its lineage row is valid, and nothing of it is stored)
   const int hyp = a.row_hyp[row];
-  if (a.done && a.done[hyp]) return;
-  const int nk = a.row_pos[row] + 1;
+  const int nk = min(a.row_pos[row] + 1, a.n_ctx);
+  float qf[8];
+  load8(a.q + (long long)row * a.ldq + h * HD + sub * 8, qf);
   const int kbeg = KSPLIT ? wv * nk / 4 : 0, kend = KSPLIT ? (wv + 1) * nk / 4 : nk;
   const int* lrow = a.lin ? a.lin + (long long)hyp * a.n_ctx : nullptr;
   const long long hstride = (long long)H * a.n_ctx * HD;
   const bf16* K = a.kbase + (long long)h * a.n_ctx * HD + sub * 8;
   const bf16* V = a.vbase + (long long)h * a.n_ctx * HD + sub * 8;
-  if (a.stat && lane == 0 && (!KSPLIT || wv == 0))
-    atomicAdd(a.stat + (pair & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
-  float qf[8];
-  load8(a.q + (long long)row * a.ldq + h * HD + sub * 8, qf);
 #pragma unroll
   for (int i = 0; i < 8; ++i) qf[i] *= a.scale_log2;
   float m = -INFINITY, l = 0.f, o[8];
@@ -616,6 +616,9 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
     }
     m = M;
   }
+  const bool dead = a.done && a.done[hyp];
+  if (a.stat && !dead && lane == 0 && (!KSPLIT || wv == 0))
+    atomicAdd(a.stat + (pair & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
   if constexpr (KSPLIT) {
     // the 4 waves' (m, l, o) merged in wave order (a wave with no keys has m = -inf, l = 0, o = 0)
     __shared__ float s_o[4][HD], s_ml[4][2];
@@ -637,14 +640,14 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
 #pragma unroll
       for (int i = 0; i < 8; ++i) O[i] += s_o[w][sub * 8 + i] * c;
     }
-    if (g == 0) {
+    if (g == 0 && !dead) {
       const float inv = 1.0f / L;
       bf16x8 r;
 #pragma unroll
       for (int i = 0; i < 8; ++i) r[i] = f2bf(O[i] * inv);
       *(bf16x8*)(a.out + (long long)row * a.ldo + h * HD + sub * 8) = r;
     }
-  } else if (g == 0) {
+  } else if (g == 0 && !dead) {
     const float inv = 1.0f / l;
     bf16x8 r;
 #pragma unroll
