@@ -446,6 +446,11 @@ def roofline_block(breakdown, prof, dom, args, beam: int = 1, traffic_json: Opti
         try:
             tj = json.load(open(tj_path))
             roof["traffic"] = tj.get(dom)
+            if roof["traffic"] is not None:
+                # not measured in this run: PMC counters need their own rocprofv3 passes (tools/pmc_traffic.sh)
+                roof["traffic_source"] = (f"{os.path.relpath(tj_path, ROOT)}: committed rocprofv3 --pmc passes "
+                                          "(FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) of this kernel on this "
+                                          "workload; HBM bytes per launch, not measured in this run")
         except Exception:
             pass
     if beam > 1 and not args.cross_fp8:
@@ -601,7 +606,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # VLOG_AMD_BENCH_SHARE_GPU=1 + VLOG_AMD_BENCH_BACKEND=gloo: a rehearsal of the N > 1 path with every rank on
+    # VLOG_AMD_BENCH_SHARE_GPU=1: a rehearsal of the N > 1 path with every rank on
     # the visible GPUs round-robin (RCCL refuses two ranks on one device; no collective is on the data path)
     if os.environ.get("VLOG_AMD_BENCH_SHARE_GPU") == "1":
         local = local % max(1, torch.cuda.device_count())
@@ -615,12 +620,11 @@ def main():
         json_fd = os.dup(1)
         os.dup2(2, 1)
         import torch.distributed as dist
-        backend = os.environ.get("VLOG_AMD_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-        host_group = dist.new_group(backend="gloo")      # host scalars (log-mel max, timing): no RCCL on the data path
+        # one gloo process group for the host scalars (log-mel max, expected-token estimates, timing): the windows
+        # shard with no device collective, so RCCL is never brought up; each rank's GPU comes from
+        # LOCAL_RANK (torch.cuda.set_device above)
+        dist.init_process_group("gloo")
+        host_group = dist.group.WORLD
 
     dims = model_dims(args.model)
     t = time.perf_counter()
@@ -714,16 +718,19 @@ def main():
         return
     toks = pipe.last["tokens"]
     mean_tok = float(np.mean(toks))
+    # BASELINE.json configs: 4 = large-v3 bf16 greedy (the headline), 5 = large-v3 beam 5 + word timestamps
+    cfg_name = ("config 4" if args.beam == 1 and not args.word_timestamps and args.model == "large-v3" else
+                "config 5" if args.beam > 1 and args.word_timestamps and args.model == "large-v3" else "non-config variant")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16+e4m3-cross" if args.cross_fp8 else "bf16",
         "data": "synthetic",
-        "config": {"workload": f"{args.model} bf16{' (opt-in fp8 e4m3 cross memory)' if args.cross_fp8 else ''} "
-                               f"{'greedy' if args.beam == 1 else 'beam%d' % args.beam}, timestamps on"
-                               f"{', word timestamps' if args.word_timestamps else ''}, "
-                               f"{W} x 30 s windows per GPU of the seeded speech-like corpus, window-sharded "
-                               f"({'config 5' if args.beam > 1 and args.word_timestamps else 'config 4' if args.beam == 1 else 'beam search'})",
+        "config": {"workload": f"{cfg_name}: {args.model} bf16{' (opt-in fp8 e4m3 cross memory)' if args.cross_fp8 else ''} "
+                               f"{'greedy' if args.beam == 1 else 'beam_size=%d' % args.beam}"
+                               f"{' + word_timestamps' if args.word_timestamps else ''}, timestamps on, "
+                               f"{W} x 30 s windows per GPU of the seeded speech-like corpus "
+                               f"({args.workload} transcript lengths), window-sharded",
                    "model": args.model, "windows_per_gpu": W, "audio_s_per_gpu_per_step": W * 30.0,
                    "mean_tokens_per_window": round(mean_tok, 1), "decoder_steps": pipe.last["steps"],
                    "token_length_min_p50_max": [int(np.min(toks)), int(np.median(toks)), int(np.max(toks))],
@@ -737,7 +744,7 @@ def main():
                    "active_row_fraction": (round(sum(n + 1 for n in pipe.last.get("all_tokens", toks))
                                                  / pipe.last["gen_stats"]["row_steps"], 4)
                                            if pipe.last["gen_stats"].get("row_steps") else None),
-                   "workload": args.workload,
+                   "corpus": args.workload,
                    "token_crc32": pipe.last["crc"],
                    "parallelism": f"window-shard x{world}",
                    "weights": (f"synthetic seed 0, random-init + planted eot_after={args.eot_after}" if args.random_weights

@@ -288,7 +288,9 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "cross_mfma_fuse" (default 0): 1 = that merge done inside the kernel by the last-arriving key split (same
  *   arithmetic and order, bit-identical output; measured ~6 % slower per cross-attention than the separate kernel).
  *   "debug_nan_row" (default -1, TEST ONLY): >= 0 overwrites logits row r of every decode pass of wm_generate with
- *   NaN before token selection (exercises the failure contract of wm_generate). */
+ *   NaN before token selection (exercises the failure contract of wm_generate).
+ *   "debug_nan_count" (default 1, TEST ONLY): the number of consecutive rows from "debug_nan_row" (a whole beam group
+ *   gives that window no live candidate). */
 int wm_set_option(wm_engine* e, const char* key, int64_t value);
 /* The engine's current value of an option (every key wm_set_option accepts, incl. environment overrides). */
 int wm_get_option(wm_engine* e, const char* key, int64_t* value);

@@ -139,11 +139,14 @@ def record(name: str, rows: List[WindowParity], **extra) -> dict:
 
 
 def source_offset(stride: int, env: str) -> int:
-    """Which residue class of windows a strided sweep covers: seeded by the tree's kernel sources (the GPU box has no
-    .git), so every change of the HIP code rotates the swept windows and every window is eventually covered (the
-    environment variable `env` overrides).  Tests record it with their results."""
+    """Which residue class of windows a strided sweep covers.  Deterministic by default (0), so the gated subset does
+    not move between commits that never touched it (ADVICE r5).  The environment variable `env` pins another class;
+    `VLOG_AMD_SWEEP_ROTATE=1` seeds it from the tree's kernel sources instead (the separate, recorded rotating sweep:
+    every change of the HIP code then covers other windows).  Tests record the offset with their results."""
     if env in os.environ:
         return int(os.environ[env]) % stride
+    if os.environ.get("VLOG_AMD_SWEEP_ROTATE") != "1":
+        return 0
     import glob
     import hashlib
     h = hashlib.sha256()

@@ -54,6 +54,26 @@ def test_nan_logits_row_raises(tiny, kw):
         assert [r.tokens for r in again] == [r.tokens for r in ok]
 
 
+def test_nan_whole_beam_group_ends_cleanly(tiny):
+    """every hypothesis of one window non-finite -> beam_select sees no live candidate (nlive 0).
+    The dead beams must take a valid lineage and token (not uninitialised LDS), the call raises with the error word,
+    and the engine decodes the same afterwards."""
+    eng, prompt, sup, W = tiny
+    kw = dict(beam_size=5)
+    ok, _ = eng.generate(list(range(W)), [prompt] * W, suppress_tokens=sup, max_length=100, **kw)
+    eng.set_option("debug_nan_row", 5)          # window 1's five hypotheses
+    eng.set_option("debug_nan_count", 5)
+    try:
+        assert eng.option("debug_nan_count") == 5
+        with pytest.raises(RuntimeError, match="non-finite"):
+            eng.generate(list(range(W)), [prompt] * W, suppress_tokens=sup, max_length=100, **kw)
+    finally:
+        eng.set_option("debug_nan_row", -1)
+        eng.set_option("debug_nan_count", 1)
+    again, _ = eng.generate(list(range(W)), [prompt] * W, suppress_tokens=sup, max_length=100, **kw)
+    assert [r.tokens for r in again] == [r.tokens for r in ok]
+
+
 def test_bad_prompt_token_raises(tiny):
     eng, prompt, sup, W = tiny
     with pytest.raises(RuntimeError, match="vocabulary"):

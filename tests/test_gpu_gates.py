@@ -247,7 +247,7 @@ def test_config4_variable_length_gates_and_row_set_decode(lv3_var):
     # every 3rd window plus the shortest and the longest transcript through the oracle (every window of the uniform
     # config 4 is gated above; VLOG_AMD_GATE_STRIDE=1 gates every window here too)
     stride = max(1, int(os.environ.get("VLOG_AMD_GATE_STRIDE", "3")))
-    offset = source_offset(stride, "VLOG_AMD_GATE_OFFSET")           # rotates with the kernel sources
+    offset = source_offset(stride, "VLOG_AMD_GATE_OFFSET")           # 0 unless pinned or VLOG_AMD_SWEEP_ROTATE=1
     lens0 = [len(r.tokens) for r in res]
     gw = sorted(set(range(offset, cfg.W, stride)) | {int(np.argmin(lens0)), int(np.argmax(lens0))})
     g = gate_windows(cfg.orc, cfg.enc_of, cfg.prompt, res, cfg.st, cfg.opt(), cfg.tok, windows=gw)

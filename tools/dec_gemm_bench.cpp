@@ -115,6 +115,8 @@ int main(int argc, char** argv) {
     const double us = timeit([&](int) { hipLaunchKernelGGL(empty_kernel, dim3(240), dim3(256), 0, st, 0); });
     std::printf("empty kernel (240 x 256)             %7.2f us\n", us);
   }
+  // DGB_BIG=1: the large-pass ring plans only (beam-group row counts): rows per block x columns x LDS budget x K range
+  const bool big_only = std::getenv("DGB_BIG") && std::atoi(std::getenv("DGB_BIG")) == 1;
   for (auto& s : shapes) {
     const double wbytes = 2.0 * s.N * s.K;
     GemmEpi ep;
@@ -148,6 +150,30 @@ int main(int argc, char** argv) {
         launch_gemm(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, st);
       });
       std::printf("%s N=%5d K=%5d  launch_gemm        %7.2f us  %7.1f GB/s(W)\n", s.name, s.N, s.K, us, wbytes / us / 1e3);
+    }
+    if (big_only) {
+      struct BigCfg { int rpb, cols, lds, kr, waves; };
+      const BigCfg cfgs[] = {{64, 64, 72, 0, 4},    {128, 64, 72, 0, 4},   {64, 32, 144, 0, 4},   {128, 128, 144, 0, 4},
+                             {128, 128, 144, 0, 8}, {128, 64, 144, 0, 8},  {128, 64, 72, 0, 8},   {64, 128, 144, 0, 8},
+                             {64, 64, 144, 0, 8},   {64, 64, 72, 0, 8},    {128, 128, 144, 640, 8}, {128, 128, 144, 1280, 8},
+                             {128, 128, 144, 2560, 8}, {128, 64, 144, 2560, 8}, {64, 128, 144, 640, 8}};
+      for (const auto& c : cfgs) {
+        const int kr = c.kr >= s.K ? 0 : c.kr;
+        if (c.kr && !kr) continue;
+        CK(hipMemsetAsync(dC, 0, cbytes, st));
+        if (!launch_dec_ring(a, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, c.rpb, c.cols, c.lds, c.waves)) {
+          std::printf("%s ring rows=%d cols=%d lds=%d kr=%d waves=%d unsupported\n", s.name, c.rpb, c.cols, c.lds, kr, c.waves);
+          continue;
+        }
+        CK(hipStreamSynchronize(st));
+        const double err = f32 ? 0.0 : maxdiff();
+        const double us = timeit([&](int r) {
+          launch_dec_ring(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, c.rpb, c.cols, c.lds, c.waves);
+        });
+        std::printf("%s N=%5d K=%5d  RING rows=%3d cols=%3d lds=%3d kr=%4d w=%d %7.2f us  %7.1f TF/s  rel diff %.1e\n", s.name,
+                    s.N, s.K, c.rpb, c.cols, c.lds, kr, c.waves, us, 2.0 * M * s.N * s.K / us / 1e6, err);
+      }
+      continue;
     }
     for (int pad : {0, 64}) {
       // pad: activation row stride K + pad (a 64-element pad moves consecutive rows to different L2 channels)

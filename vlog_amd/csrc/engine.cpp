@@ -185,6 +185,7 @@ struct wm_engine {
   DevBuf d_win_prompt, d_win_slot, d_hyp_out, d_res_tok, d_res_len, d_res_cum, d_res_ns, d_res_lp, d_res_lp_o, d_ev;
   std::vector<int> h_ev;     // host image of d_ev (kept alive until the next poll syncs the stream)
   int dbg_nan_row = -1;      // TEST ONLY (wm_set_option "debug_nan_row"): NaN logits row before every selection
+  int dbg_nan_count = 1;     // TEST ONLY ("debug_nan_count"): rows [debug_nan_row, + count) (a whole beam group: nlive 0)
   // step activations
   DevBuf s_x, s_hb, s_q, s_ao, s_ff, s_logits, s_pm, s_pl, s_po;
   // profiler: per class, HIP event pairs recorded on the launch stream + algorithmic flops / bytes
@@ -1006,10 +1007,12 @@ void upload_suppress(wm_engine* e, const wm_generate_args* a, hipStream_t st) {
   HIP_OK(hipStreamSynchronize(st));
 }
 
-// TEST ONLY (option debug_nan_row): NaN into one logits row before selection (bytes 0xFF are a NaN)
+// TEST ONLY (options debug_nan_row / debug_nan_count): NaN into logits rows before selection (bytes 0xFF are a NaN)
 void debug_nan(wm_engine* e, float* logits, int rows, hipStream_t s) {
-  if (e->dbg_nan_row >= 0 && e->dbg_nan_row < rows)
-    HIP_OK(hipMemsetAsync(logits + (size_t)e->dbg_nan_row * e->dm.n_vocab, 0xFF, (size_t)e->dm.n_vocab * 4, s));
+  if (e->dbg_nan_row >= 0 && e->dbg_nan_row < rows) {
+    const int n = std::min(e->dbg_nan_count, rows - e->dbg_nan_row);
+    HIP_OK(hipMemsetAsync(logits + (size_t)e->dbg_nan_row * e->dm.n_vocab, 0xFF, (size_t)n * e->dm.n_vocab * 4, s));
+  }
 }
 
 // One graph-replayed decode loop's capture state (see generate)
@@ -2123,8 +2126,8 @@ void align_batch(wm_engine* e, int n, const int* h_slots, int sot_len, const int
       const int it = ord[i1];
       const int s2 = std::max(smax, S[it]);
       // per item: its attention capture, the factored form's K/V gather, and the fused alignment's f64 statistics
-      // (n_heads x F x 2 doubles, F <= T / 2)
-      const double bytes = (double)(i1 - i0 + 1) * (s2 * n_heads * T * 4 + per_item_kv + (double)n_heads * T * 8) +
+      // (n_heads x F x 2 doubles, F <= T: the buffer is c x n_heads x fmax x 16 bytes)
+      const double bytes = (double)(i1 - i0 + 1) * (s2 * n_heads * T * 4 + per_item_kv + (double)n_heads * T * 16) +
                            (double)(ntext + nt[it]) * V * 4;
       if (i1 > i0 && (bytes > budget || (double)(i1 - i0 + 1) * s2 > 1.25 * (double)(sum_s + S[it]))) break;
       smax = s2;
@@ -2651,6 +2654,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
       }
     }
     else if (k == "debug_nan_row") e->dbg_nan_row = (int)std::max<int64_t>(-1, std::min<int64_t>(value, 1 << 30));
+    else if (k == "debug_nan_count") e->dbg_nan_count = (int)std::max<int64_t>(1, std::min<int64_t>(value, 1 << 20));
     else if (k == "cross_tf") e->cross_tf = value ? 1 : 0;
     else if (k == "cross_mfma") e->cross_mfma = value ? 1 : 0;
     else if (k == "cross_mfma_fuse") e->cross_mfma_fuse = value ? 1 : 0;
@@ -2700,6 +2704,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_fp8") *value = e->cross_fp8;
     else if (k == "cross_mode") *value = e->cross_mode;
     else if (k == "debug_nan_row") *value = e->dbg_nan_row;
+    else if (k == "debug_nan_count") *value = e->dbg_nan_count;
     else if (k == "cross_tf") *value = e->cross_tf;
     else if (k == "cross_mfma") *value = e->cross_mfma;
     else if (k == "cross_mfma_fuse") *value = e->cross_mfma_fuse;

@@ -94,8 +94,10 @@ void launch_splitk_combine(const float* part, int splitk, int M, int N, const Ge
 // rows_per_block > 0: the rows are split into groups of that many (32..160) — one block per (32-column tile, row
 // group, K split); the row groups of a tile share its weight panel through one XCD's L2 (any M).  lds_kb: the ring's
 // LDS budget, 144 (one block per CU) or 72 (two resident blocks per CU); 0 = the process default (VLOG_AMD_RING_LDS).
+// waves: 4, or 8 (64 / 128 rows x 64 / 128 columns per block: two waves per SIMD).
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block = 0, int cols = 32, int lds_kb = 0);
+                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block = 0, int cols = 32, int lds_kb = 0,
+                     int waves = 4);
 // Folded-LayerNorm vectors of a consumer projection (gemm_dec.hip): s = W g, c = W b + bias (f64 sums, f32 out).
 void launch_fold_vectors(const bf16* w, int N, int K, const float* g, const float* b, const float* bias, float* s_out,
                          float* c_out, hipStream_t st);

@@ -188,15 +188,20 @@ __device__ __forceinline__ void vm_wait(int n) {
 // LNF: the folded-LayerNorm consumer (GemmA.fold_*): its row-sum loads are issued before the ring's first panels and
 // reduced after the last one (the epilogue is their only reader), in a separate instantiation so the plain kernel's
 // pipeline is untouched (a runtime-gated prologue made the compiler drain the DMA queue: 1.6x slower at 750 rows).
-template <int MF, int KIND, int R, int PK = 1, int NC = 1, bool LNF = false>
-__global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
-                                                       int K, GemmEpi epi, int tiles_n, int splitk, int kr,
-                                                       float* __restrict__ part, int rgroups) {
-  static_assert(MF % 2 == 0, "MF must be even");
+// NW = 4 or 8 waves: 2 column halves x NW / 2 row slices.  Eight waves halve each wave's LDS-DMA issue and fragment
+// reads per sub-panel and put two waves on every SIMD, so one wave's DMA issue and barrier wait overlap the other's
+// MFMAs (at 750 rows the 4-wave block was bound by its own per-wave DMA issue, not by the L2).
+template <int MF, int KIND, int R, int PK = 1, int NC = 1, bool LNF = false, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void dec_ring_kernel(GemmA a, const bf16* __restrict__ w, long long ldw, int M, int N,
+                                                           int K, GemmEpi epi, int tiles_n, int splitk, int kr,
+                                                           float* __restrict__ part, int rgroups) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(!LNF || NW == 4, "the folded-LayerNorm statistics split assumes 256 threads");
   // a ring slot holds PK consecutive 64-k sub-panels (one barrier per PK x 64 of K); a block covers WR = 32 NC
-  // output columns (each wave NC fragments of 16)
-  constexpr int ROWS = MF * 16, HALF = MF / 2, WR = 32 * NC, SUB = (ROWS + WR) * 64, SLOT = PK * SUB, DA = ROWS / 32,
-                DPP = PK * (DA + NC);
+  // output columns (each wave NC fragments of 16) and ROWS rows (each wave HALF fragments of 16: its row slice)
+  constexpr int WRS = NW / 2, ROWS = MF * 16, HALF = MF / WRS, WR = 32 * NC, SUB = (ROWS + WR) * 64, SLOT = PK * SUB,
+                DA = ROWS / (8 * NW), NCW = NC * 4 / NW, DPP = PK * (DA + NCW);
+  static_assert(MF % WRS == 0 && ROWS % (8 * NW) == 0 && (NC * 4) % NW == 0, "tile does not split over the waves");
   __shared__ __attribute__((aligned(16))) bf16 smem[R * SLOT];
   __shared__ float sMR[2][LNF ? ROWS : 1];              // folded LayerNorm: rstd and rstd * mean per row
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -233,21 +238,21 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
       pfc[c] = *(const f32x4*)(epi.fold_c + col0);
     }
   }
-  // DMA sources: wave `wid` moves A rows [wid*ROWS/4, +ROWS/4) (DA instructions of 8 rows) and W rows
-  // [8 NC wid, +8 NC) (NC instructions)
+  // DMA sources: wave `wid` moves A rows [wid*ROWS/NW, +ROWS/NW) (DA instructions of 8 rows) and W rows
+  // [8 NCW wid, +8 NCW) (NCW instructions)
   const bf16* srcA[DA];
 #pragma unroll
   for (int j = 0; j < DA; ++j) {
-    const int row = wid * (ROWS / 4) + j * 8 + (lane >> 3);
+    const int row = wid * (ROWS / NW) + j * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
     const int gr = min(m0 + row, M - 1);
     const long long off = a.rpb ? (long long)(gr / a.rpb) * a.bstride + (long long)(gr % a.rpb) * a.ld : (long long)gr * a.ld;
     srcA[j] = a.ptr + off + kb + ch * 8;
   }
-  const bf16* srcW[NC];
+  const bf16* srcW[NCW];
 #pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    const int row = (wid * NC + j) * 8 + (lane >> 3);
+  for (int j = 0; j < NCW; ++j) {
+    const int row = (wid * NCW + j) * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
     srcW[j] = w + (long long)min(n0 + row, N - 1) * ldw + kb + ch * 8;
   }
@@ -260,11 +265,11 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(GemmA a, const bf16* __re
 #pragma unroll
       for (int j = 0; j < DA; ++j)
         __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + sp * 64),
-                                         (__attribute__((address_space(3))) void*)(s + (wid * (ROWS / 4) + j * 8) * 64), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(s + (wid * (ROWS / NW) + j * 8) * 64), 16, 0, 0);
 #pragma unroll
-      for (int j = 0; j < NC; ++j)
+      for (int j = 0; j < NCW; ++j)
         __builtin_amdgcn_global_load_lds((const void*)(srcW[j] + sp * 64),
-                                         (__attribute__((address_space(3))) void*)(s + (ROWS + (wid * NC + j) * 8) * 64), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(s + (ROWS + (wid * NCW + j) * 8) * 64), 16, 0, 0);
     }
   };
 
@@ -403,7 +408,7 @@ static int ring_lds_kb() {
   return v;
 }
 
-template <int MF, int KIND, int NC, int CAPKB, bool LNF>
+template <int MF, int KIND, int NC, int CAPKB, bool LNF, int NW = 4>
 static void run_ring_cap_f(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                          int splitk, int kr, hipStream_t st) {
   constexpr int SUBB = (MF * 16 + 32 * NC) * 128;      // bytes of one 64-k sub-panel
@@ -416,7 +421,7 @@ static void run_ring_cap_f(const GemmA& a, const bf16* w, long long ldw, int M, 
   const int pk = ring_pk();
   if constexpr (R4 >= 3) {
     if (pk == 4) {
-      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R4, 4, NC, LNF>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R4, 4, NC, LNF, NW>), grid, dim3(NW * 64), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
                          splitk, kr, ws, rgroups);
       WM_LAUNCH_CHECK("dec_ring_kernel");
       return;
@@ -424,21 +429,28 @@ static void run_ring_cap_f(const GemmA& a, const bf16* w, long long ldw, int M, 
   }
   if constexpr (R2 >= 3) {
     if (pk >= 2) {
-      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R2, 2, NC, LNF>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
+      hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R2, 2, NC, LNF, NW>), grid, dim3(NW * 64), 0, st, a, w, ldw, M, N, K, epi, tiles_n,
                          splitk, kr, ws, rgroups);
       WM_LAUNCH_CHECK("dec_ring_kernel");
       return;
     }
   }
   static_assert(R * SUBB <= 160 * 1024, "ring exceeds the LDS");
-  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R, 1, NC, LNF>), grid, dim3(256), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk,
+  hipLaunchKernelGGL((dec_ring_kernel<MF, KIND, R, 1, NC, LNF, NW>), grid, dim3(NW * 64), 0, st, a, w, ldw, M, N, K, epi, tiles_n, splitk,
                      kr, ws, rgroups);
   WM_LAUNCH_CHECK("dec_ring_kernel");
 }
 
 template <int MF, int KIND, int NC, int CAPKB>
 static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                         int splitk, int kr, hipStream_t st) {
+                         int splitk, int kr, hipStream_t st, int waves) {
+  if constexpr (MF % 4 == 0 && MF * 16 % 64 == 0 && NC % 2 == 0) {
+    if (waves == 8 && !a.fold_stat) {
+      run_ring_cap_f<MF, KIND, NC, CAPKB, false, 8>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+      return;
+    }
+  }
+  if (waves == 8) throw std::runtime_error("dec_ring: 8 waves need 64 or 128 rows x 64 or 128 columns, no folded LayerNorm");
   if constexpr (KIND == EPI_BF16 || KIND == EPI_DEC_QKV) {
     if (a.fold_stat) {
       run_ring_cap_f<MF, KIND, NC, CAPKB, true>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
@@ -450,29 +462,35 @@ static void run_ring_cap(const GemmA& a, const bf16* w, long long ldw, int M, in
 
 template <int MF, int KIND, int NC>
 static void run_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     int splitk, int kr, hipStream_t st, int lds_kb) {
-  if ((lds_kb > 0 ? lds_kb : ring_lds_kb()) == 72) run_ring_cap<MF, KIND, NC, 72>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
-  else run_ring_cap<MF, KIND, NC, 144>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st);
+                     int splitk, int kr, hipStream_t st, int lds_kb, int waves) {
+  if ((lds_kb > 0 ? lds_kb : ring_lds_kb()) == 72) run_ring_cap<MF, KIND, NC, 72>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, waves);
+  else run_ring_cap<MF, KIND, NC, 144>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, waves);
 }
 
 // rows_per_block 0: one row group covering every row (MF from M); else 32 / 64 / 96 / 128 / 160 rows per block
 // and ceil(M / rows) row groups.
 template <int KIND>
 static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi,
-                          float* ws, int splitk, int kr, int rows_per_block, int cols, hipStream_t st, int lds_kb) {
+                          float* ws, int splitk, int kr, int rows_per_block, int cols, hipStream_t st, int lds_kb, int waves) {
   const int rows = rows_per_block > 0 ? std::min(rows_per_block, ((M + 31) / 32) * 32) : M;
+  if (cols == 128) {                     // 128-column tiles (waves of 64 columns): row groups of 64 or 128
+    if (rows <= 64) run_ring<4, KIND, 4>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+    else if (rows <= 128) run_ring<8, KIND, 4>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+    else throw std::runtime_error("dec_ring: 128-column tiles take at most 128 rows per block");
+    return;
+  }
   if (cols == 64) {                      // 64-column tiles: row groups of 32, 64 or 128
-    if (rows <= 32) run_ring<2, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
-    else if (rows <= 64) run_ring<4, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
-    else if (rows <= 128) run_ring<8, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+    if (rows <= 32) run_ring<2, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+    else if (rows <= 64) run_ring<4, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+    else if (rows <= 128) run_ring<8, KIND, 2>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
     else throw std::runtime_error("dec_ring: 64-column tiles take at most 128 rows per block");
     return;
   }
-  if (rows <= 32) run_ring<2, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
-  else if (rows <= 64) run_ring<4, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
-  else if (rows <= 96) run_ring<6, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
-  else if (rows <= 128) run_ring<8, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
-  else run_ring<10, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb);
+  if (rows <= 32) run_ring<2, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+  else if (rows <= 64) run_ring<4, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+  else if (rows <= 96) run_ring<6, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+  else if (rows <= 128) run_ring<8, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
+  else run_ring<10, KIND, 1>(a, w, ldw, M, N, K, epi, ws, splitk, kr, st, lds_kb, waves);
 }
 
 // Ring path: N % 4 == 0, K % 64 == 0; M <= 160 for one row group, any M with rows_per_block > 0.  kr = K range
@@ -480,11 +498,17 @@ static void dispatch_ring(const GemmA& a, const bf16* w, long long ldw, int M, i
 // 32 or 64 (64: at most 64 rows per block).  A column tile's width never changes a row's K summation order, so
 // both widths give bit-identical results.  Returns false when unsupported.
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block, int cols, int lds_kb) {
+                     size_t ws_bytes, int kr, hipStream_t st, int rows_per_block, int cols, int lds_kb, int waves) {
   if (lds_kb != 0 && lds_kb != 72 && lds_kb != 144) return false;
+  if (waves != 4 && waves != 8) return false;
+  if (waves == 8) {                      // 8 waves: 64 / 128 rows per block x 64 / 128 columns, no folded LayerNorm
+    const int rows = rows_per_block > 0 ? std::min(rows_per_block, ((M + 31) / 32) * 32) : M;
+    if (cols < 64 || !(rows > 32 && rows <= 128) || a.fold_stat) return false;
+  }
   if ((rows_per_block <= 0 && M > 160) || rows_per_block > 160 || N % 4 != 0 || K % 64 != 0) return false;
-  if (cols != 32 && cols != 64) return false;
-  if (cols == 64 && (rows_per_block <= 0 ? M : std::min(rows_per_block, ((M + 31) / 32) * 32)) > 128) return false;
+  if (cols != 32 && cols != 64 && cols != 128) return false;
+  if (cols >= 64 && (rows_per_block <= 0 ? M : std::min(rows_per_block, ((M + 31) / 32) * 32)) > 128) return false;
+  if (cols == 128 && lds_kb == 72) return false;        // a 128 x 128 sub-panel is 32 KiB: two slots would be all of it
   if (kr <= 0) kr = K <= 1280 ? K : ((K + (K + 1279) / 1280 - 1) / ((K + 1279) / 1280) + 63) / 64 * 64;
   if (kr % 64 != 0) return false;
   const int splitk = (K + kr - 1) / kr;
@@ -497,11 +521,11 @@ bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N,
   if (epi.xg_out && (epi.kind != EPI_RESID_F32 || N % 16 != 0 || !epi.stat_out || !epi.bias || !epi.xg_g)) return false;
   if (!slab && (epi.ldc % 4 != 0 || (epi.rpb != 0 && epi.bstride % 4 != 0))) return false;
   switch (epi.kind) {
-    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
-    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
-    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
-    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
-    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb); break;
+    case EPI_BF16: dispatch_ring<EPI_BF16>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb, waves); break;
+    case EPI_RESID_F32: dispatch_ring<EPI_RESID_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb, waves); break;
+    case EPI_F32: dispatch_ring<EPI_F32>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb, waves); break;
+    case EPI_DEC_QKV: dispatch_ring<EPI_DEC_QKV>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb, waves); break;
+    case EPI_RESID_LN: dispatch_ring<EPI_RESID_LN>(a, w, ldw, M, N, K, epi, ws, splitk, kr, rows_per_block, cols, st, lds_kb, waves); break;
     default: return false;
   }
   if (slab && !epi.defer_combine) launch_splitk_combine(ws, splitk, M, N, epi, st);

@@ -620,6 +620,11 @@ __global__ __launch_bounds__(256) void beam_select_kernel(BeamParams p) {
         s_par[nlive] = o_src[c]; s_new[nlive] = o_tk[c]; s_sc[nlive] = o_sc[c]; ++nlive;
       }
     }
+    if (nlive == 0) {
+      // no live candidate (every candidate non-finite or finished): the dead beams below copy beam 0's lineage and a
+      // valid token, so no later pass reads a hypothesis index or token from uninitialised LDS
+      s_par[0] = 0; s_new[0] = p.eot; s_sc[0] = -INFINITY;
+    }
     p.n_fin[w] = nf;
     s_nlive = nlive;
     s_nf_new = nnew;
