@@ -2,8 +2,9 @@
 64-row ring-GEMM route at its two LDS budgets ("decode_gemm_big_lds" 72 = two resident blocks per CU, the default,
 and 144 = one) must give the same bits — the ring depth never changes a row's K summation order — and the same
 tokens as the route below the threshold.  Beam 5 over 110 windows of the margin-planted tiny model (550 rows), over
-64 (320 rows) and over 40 (200 rows, above the default threshold of 161); at 550 rows also the opt-in 128-row groups
-("VLOG_AMD_DEC_BIG128", process-wide, so not switched here) are covered only by tools/dec_gemm_bench's comparison."""
+64 (320 rows) and over 40 (200 rows, above the default threshold of 161).  The 8-wave plan ("decode_gemm_big128":
+128 x 64 / 128 x 128 / 64 x 64 tiles of 8 waves) walks every row's K in the same order, so it must give the same
+bits too."""
 import numpy as np
 import pytest
 import torch
@@ -53,8 +54,11 @@ def test_big_rows_lds_budgets_bit_identical(setup):
         a = _beam(eng, enc, tok, n=n, decode_gemm_big_lds=72)
         b = _beam(eng, enc, tok, n=n, decode_gemm_big_lds=144)
         c = _beam(eng, enc, tok, n=n, decode_gemm_big_rows=0)    # the route below the threshold
+        d = _beam(eng, enc, tok, n=n, decode_gemm_big128=161)    # the 8-wave plan on every big pass
         assert [r.tokens for r in a] == [r.tokens for r in b], n
         assert [r.score for r in a] == [r.score for r in b], n  # bit for bit
+        assert [r.tokens for r in a] == [r.tokens for r in d], n
+        assert [r.score for r in a] == [r.score for r in d], n  # bit for bit
         assert [r.tokens for r in a] == [r.tokens for r in c], n
         assert max(abs(x.score - y.score) for x, y in zip(a, c)) < 2e-3, n
         if n == W:

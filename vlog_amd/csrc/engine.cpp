@@ -230,9 +230,11 @@ struct wm_engine {
                              // costs ~3 round trips, more than the combine kernel behind it in the stream)
   int dec_big_rows = 161;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
                              // whole K per block (decoder_layer); 320 before the two-blocks-per-CU tiles below
-  int dec_big128 = 0;        // ... from this many rows qkv / fc1 / fc2 in 128-row groups (0: never; VLOG_AMD_DEC_BIG128).
-                             // Off: faster alone (dec_gemm_bench, 750 rows) but slower in the step (config 5, arms
-                             // alternating on one box: dec_gemm 605 vs 566 ms per step, profiles/ab_r04_c5_big128.txt)
+  int dec_big128 = 0;        // ... from this many rows the 8-wave ring plan (0: never; VLOG_AMD_DEC_BIG128): qkv as
+                             // 128 x 64 tiles (two blocks per CU), fc1 / fc2 as 128 x 128 tiles, the d x d projections
+                             // as 64 x 64 tiles, one block of 8 waves per CU (tools/dec_gemm_bench at 640 / 750 rows,
+                             // profiles/dgb_r06_*.txt: the layer 103.5 -> 86 us at 750 rows).  (Round 4's 4-wave
+                             // 128-row groups were faster alone but slower in the step: profiles/ab_r04_c5_big128.txt)
   int dec_ln_fold = 0;       // ring passes (33..1024 rows): LayerNorms folded into their consumers (no combine launch
                              // after out / cout; fc2's combine writes stats instead of the LayerNorm).  Off: the
                              // consumers' epilogue costs more than the two launches it removes (dec_gemm 336 vs 319
@@ -595,19 +597,28 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     // (384 rows: 76 vs 86 us per layer for the 150-row plan; 750 rows: 114 vs 159 us)
     const int tr = sl.total_rows;
     const bool big = e->dec_big_rows > 0 && tr >= e->dec_big_rows && tr <= 1024;
-    // (opt-in dec_big128: qkv / fc1 / fc2 in 128-row groups, 750 rows two blocks per CU 17.2 / 18.4 / 25.6 us against
+    // (dec_big128 from round 6: the 8-wave plan below; round 4's form, qkv / fc1 / fc2 in 4-wave 128-row groups,
+    // two blocks per CU at 750 rows: 17.2 / 18.4 / 25.6 us against
     // 18.9 / 21.0 / 32.8 for 64-row groups in tools/dec_gemm_bench, yet slower inside the decode step)
     const bool sq = proj == DEC_OUT || proj == DEC_CQ || proj == DEC_COUT;
-    const int p = big ? ((e->dec_big128 > 0 && tr >= e->dec_big128 && !sq) ? 128 : 64) : plan_of(proj);
+    const bool b128 = big && e->dec_big128 > 0 && tr >= e->dec_big128;
+    int p = big ? 64 : plan_of(proj);
     // the three d x d projections keep 32-column tiles below 512 rows and one block per CU (144 KiB); qkv / fc1 / fc2
     // take 64 x 64 tiles, two blocks per CU (dec_big_lds; tools/dec_gemm_bench at 256 / 384 / 750 rows,
     // profiles/dec_gemm_bench_r04_*rows_lds*.txt)
-    const int cols = big ? ((tr >= 512 || !sq) ? 64 : 32) : e->dec_cols[proj];
-    const int lds = big ? (sq ? 144 : e->dec_big_lds) : 0;
+    int cols = big ? ((tr >= 512 || !sq) ? 64 : 32) : e->dec_cols[proj];
+    int lds = big ? (sq ? 144 : e->dec_big_lds) : 0;
+    int waves = 4;
+    if (b128) {                            // the 8-wave plan (dec_big128)
+      waves = 8;
+      if (sq) { p = 64; cols = 64; lds = 144; }
+      else if (proj == DEC_QKV) { p = 128; cols = 64; lds = 72; }
+      else { p = 128; cols = 128; lds = 144; }
+    }
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
     const int kr = e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 || big ? K : 1280);
-    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols, lds)) return;
+    if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols, lds, waves)) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
     if (a.fold_stat || ep.xg_out) throw std::runtime_error("decoder: a folded-LayerNorm projection left the ring path");
@@ -2659,6 +2670,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_mfma") e->cross_mfma = value ? 1 : 0;
     else if (k == "cross_mfma_fuse") e->cross_mfma_fuse = value ? 1 : 0;
     else if (k == "decode_gemm_big_rows") e->dec_big_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
+    else if (k == "decode_gemm_big128") e->dec_big128 = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
     else if (k == "decode_ln_fold") e->dec_ln_fold = value ? 1 : 0;
     else if (k == "decode_gemm_big_lds") {
       if (value != 72 && value != 144) throw std::runtime_error("decode_gemm_big_lds: 72 or 144");
@@ -2709,6 +2721,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_mfma") *value = e->cross_mfma;
     else if (k == "cross_mfma_fuse") *value = e->cross_mfma_fuse;
     else if (k == "decode_gemm_big_rows") *value = e->dec_big_rows;
+    else if (k == "decode_gemm_big128") *value = e->dec_big128;
     else if (k == "decode_ln_fold") *value = e->dec_ln_fold;
     else if (k == "decode_gemm_big_lds") *value = e->dec_big_lds;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
