@@ -254,9 +254,11 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "decode_gemm_big_rows" (default 161): passes of at least this many rows (<= 1024; beam groups of many windows)
  *   route every projection to 64-row ring groups over its whole K (64 columns for qkv / fc1 / fc2, and for all from
  *   512 rows; 0 disables).  Results agree to f32 rounding.
- *   "decode_gemm_big128" (default 0 = never): passes of at least this many rows on that route take the 8-wave plan:
- *   qkv as 128-row x 64-column blocks (two per CU), fc1 / fc2 as 128 x 128, the d x d projections as 64 x 64 (one block
- *   of 8 waves per CU).  Bit-identical to the 4-wave route (same K order per row).
+ *   "decode_gemm_big128" (default 512; 0 = never): passes of at least this many rows on that route take the 8-wave
+ *   plan: qkv, fc1 and fc2 as 128-row x 128-column blocks, the d x d projections as 64 x 64 (one block of 8 waves per
+ *   CU).  Bit-identical to the 4-wave route (same K order per row) except fc2's K ranges below.
+ *   "decode_gemm_big_fc2_kr" (default 1280): fc2's K range per block on the 8-wave plan (0 = the whole K, bit-identical
+ *   to the 4-wave route; a split sums its slabs in the residual + LayerNorm combine: f32 rounding).
  *   "decode_gemm_big_lds" (default 72): LDS budget in KiB of the qkv / fc1 / fc2 ring blocks on that route, 72 (two
  *   resident blocks per CU) or 144 (one; the d x d projections always take 144).  Bit-identical either way.
  *   "decode_ln_fold" (default 0; measured slower, kept for A/B): passes of 33..1024 rows whose projections all take the ring route fold each

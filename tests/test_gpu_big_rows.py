@@ -51,14 +51,19 @@ def test_big_rows_lds_budgets_bit_identical(setup):
     dims, eng, enc, tok = setup
     assert eng.option("decode_gemm_big_lds") == 72 and eng.option("decode_gemm_big_rows") == 161
     for n in (W, 64, 40):
-        a = _beam(eng, enc, tok, n=n, decode_gemm_big_lds=72)
-        b = _beam(eng, enc, tok, n=n, decode_gemm_big_lds=144)
-        c = _beam(eng, enc, tok, n=n, decode_gemm_big_rows=0)    # the route below the threshold
-        d = _beam(eng, enc, tok, n=n, decode_gemm_big128=161)    # the 8-wave plan on every big pass
+        a = _beam(eng, enc, tok, n=n, decode_gemm_big_lds=72, decode_gemm_big128=0)     # the 4-wave route
+        b = _beam(eng, enc, tok, n=n, decode_gemm_big_lds=144, decode_gemm_big128=0)
+        c = _beam(eng, enc, tok, n=n, decode_gemm_big_rows=0)    # the route below the threshold (150-row plan)
+        # the 8-wave plan on every big pass: with fc2 over its whole K the same bits; with fc2's K in ranges (its default)
+        # the slabs are summed by the combine, so the same tokens and scores to f32 rounding
+        d = _beam(eng, enc, tok, n=n, decode_gemm_big128=161, decode_gemm_big_fc2_kr=0)
+        e = _beam(eng, enc, tok, n=n, decode_gemm_big128=161)
         assert [r.tokens for r in a] == [r.tokens for r in b], n
         assert [r.score for r in a] == [r.score for r in b], n  # bit for bit
         assert [r.tokens for r in a] == [r.tokens for r in d], n
         assert [r.score for r in a] == [r.score for r in d], n  # bit for bit
+        assert [r.tokens for r in a] == [r.tokens for r in e], n
+        assert max(abs(x.score - y.score) for x, y in zip(a, e)) < 2e-3, n
         assert [r.tokens for r in a] == [r.tokens for r in c], n
         assert max(abs(x.score - y.score) for x, y in zip(a, c)) < 2e-3, n
         if n == W:

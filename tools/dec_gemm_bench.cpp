@@ -81,20 +81,24 @@ int main(int argc, char** argv) {
   std::vector<uint16_t> hA(maxA), hW(maxW);
   for (auto& v : hA) v = f2b(U(rng));
   for (auto& v : hW) v = f2b(U(rng) * 0.05f);
-  // a distinct W copy per shape x 8 so back-to-back launches stream from HBM, not from the 256 MB MALL
-  const int NCOPY = 8;
+  // distinct W copies rotated over the launches: 8 (default) stream from the 256 MB MALL; DGB_COPIES=40 puts every
+  // launch's weights beyond it (cold, from HBM, as in a decode step, where 1.5 GB of weights cycle per pass)
+  const int NCOPY = std::getenv("DGB_COPIES") ? std::max(1, std::atoi(std::getenv("DGB_COPIES"))) : 8;
   bf16 *dA, *dW;
   void *dC, *dRef;
   float* ws;
   unsigned* sink;
   const size_t wsb = 64ull << 20;
-  CK(hipMalloc(&dA, maxA * 2));
+  // DGB_ACOPIES=n: n activation copies rotated with the weights (the big-rows sweep): each launch's A is then cold in
+  // L2 and served from the MALL, as in a decode step where the previous kernel wrote it from every XCD
+  const int ACOPY = std::getenv("DGB_ACOPIES") ? std::max(1, std::atoi(std::getenv("DGB_ACOPIES"))) : 1;
+  CK(hipMalloc(&dA, maxA * 2 * ACOPY));
   CK(hipMalloc(&dW, maxW * 2 * NCOPY));
   CK(hipMalloc(&dC, maxC * 4));
   CK(hipMalloc(&dRef, maxC * 4));
   CK(hipMalloc(&ws, wsb));
   CK(hipMalloc(&sink, 16));
-  CK(hipMemcpy(dA, hA.data(), maxA * 2, hipMemcpyHostToDevice));
+  for (int c = 0; c < ACOPY; ++c) CK(hipMemcpy(dA + maxA * c, hA.data(), maxA * 2, hipMemcpyHostToDevice));
   for (int c = 0; c < NCOPY; ++c) CK(hipMemcpy(dW + maxW * c, hW.data(), maxW * 2, hipMemcpyHostToDevice));
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -116,7 +120,9 @@ int main(int argc, char** argv) {
     std::printf("empty kernel (240 x 256)             %7.2f us\n", us);
   }
   // DGB_BIG=1: the large-pass ring plans only (beam-group row counts): rows per block x columns x LDS budget x K range
-  const bool big_only = std::getenv("DGB_BIG") && std::atoi(std::getenv("DGB_BIG")) == 1;
+  // DGB_BIG=2: the same sweep over the 150-row plan's tiles and their 8-wave alternatives
+  const int big_mode = std::getenv("DGB_BIG") ? std::atoi(std::getenv("DGB_BIG")) : 0;
+  const bool big_only = big_mode == 1 || big_mode == 2;
   for (auto& s : shapes) {
     const double wbytes = 2.0 * s.N * s.K;
     GemmEpi ep;
@@ -156,8 +162,16 @@ int main(int argc, char** argv) {
       const BigCfg cfgs[] = {{64, 64, 72, 0, 4},    {128, 64, 72, 0, 4},   {64, 32, 144, 0, 4},   {128, 128, 144, 0, 4},
                              {128, 128, 144, 0, 8}, {128, 64, 144, 0, 8},  {128, 64, 72, 0, 8},   {64, 128, 144, 0, 8},
                              {64, 64, 144, 0, 8},   {64, 64, 72, 0, 8},    {128, 128, 144, 640, 8}, {128, 128, 144, 1280, 8},
-                             {128, 128, 144, 2560, 8}, {128, 64, 144, 2560, 8}, {64, 128, 144, 640, 8}};
-      for (const auto& c : cfgs) {
+                             {128, 128, 144, 2560, 8}, {128, 64, 144, 2560, 8}, {64, 128, 144, 640, 8},
+                             {64, 64, 72, 2560, 4},  {64, 64, 72, 1280, 4},  {64, 64, 72, 2560, 8}, {128, 64, 72, 1280, 8},
+                             {128, 64, 72, 2560, 8}};
+      const BigCfg cfgs150[] = {{96, 32, 144, 0, 4}, {32, 32, 144, 0, 4}, {64, 64, 144, 0, 4}, {64, 64, 144, 1280, 4},
+                                {64, 64, 144, 0, 8}, {64, 64, 72, 0, 8}, {64, 64, 72, 0, 4}, {128, 64, 144, 0, 8},
+                                {128, 64, 72, 0, 8}, {64, 128, 144, 0, 8}, {64, 64, 144, 1280, 8}, {64, 64, 72, 1280, 8},
+                                {128, 64, 72, 1280, 8}, {32, 64, 144, 0, 4}, {64, 32, 144, 0, 4}};
+      const int ncfg = big_mode == 2 ? (int)(sizeof(cfgs150) / sizeof(cfgs150[0])) : (int)(sizeof(cfgs) / sizeof(cfgs[0]));
+      for (int ci = 0; ci < ncfg; ++ci) {
+        const BigCfg& c = big_mode == 2 ? cfgs150[ci] : cfgs[ci];
         const int kr = c.kr >= s.K ? 0 : c.kr;
         if (c.kr && !kr) continue;
         CK(hipMemsetAsync(dC, 0, cbytes, st));
@@ -168,7 +182,9 @@ int main(int argc, char** argv) {
         CK(hipStreamSynchronize(st));
         const double err = f32 ? 0.0 : maxdiff();
         const double us = timeit([&](int r) {
-          launch_dec_ring(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, c.rpb, c.cols, c.lds, c.waves);
+          GemmA ar = a;
+          ar.ptr = dA + maxA * (r % ACOPY);
+          launch_dec_ring(ar, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, c.rpb, c.cols, c.lds, c.waves);
         });
         std::printf("%s N=%5d K=%5d  RING rows=%3d cols=%3d lds=%3d kr=%4d w=%d %7.2f us  %7.1f TF/s  rel diff %.1e\n", s.name,
                     s.N, s.K, c.rpb, c.cols, c.lds, kr, c.waves, us, 2.0 * M * s.N * s.K / us / 1e6, err);

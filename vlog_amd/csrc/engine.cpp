@@ -230,11 +230,13 @@ struct wm_engine {
                              // costs ~3 round trips, more than the combine kernel behind it in the stream)
   int dec_big_rows = 161;    // passes of >= this many rows (beam groups of many windows): 64-row ring groups, the
                              // whole K per block (decoder_layer); 320 before the two-blocks-per-CU tiles below
-  int dec_big128 = 0;        // ... from this many rows the 8-wave ring plan (0: never; VLOG_AMD_DEC_BIG128): qkv as
-                             // 128 x 64 tiles (two blocks per CU), fc1 / fc2 as 128 x 128 tiles, the d x d projections
-                             // as 64 x 64 tiles, one block of 8 waves per CU (tools/dec_gemm_bench at 640 / 750 rows,
-                             // profiles/dgb_r06_*.txt: the layer 103.5 -> 86 us at 750 rows).  (Round 4's 4-wave
-                             // 128-row groups were faster alone but slower in the step: profiles/ab_r04_c5_big128.txt)
+  int dec_big128 = 512;      // ... from this many rows the 8-wave ring plan (0: never; VLOG_AMD_DEC_BIG128): qkv, fc1
+                             // and fc2 as 128 x 128 tiles (fc2's K of 4d in ranges of dec_big_fc2_kr), the d x d
+                             // projections as 64 x 64 tiles, one block of 8 waves per CU.  Config 5 (750 rows): dec_gemm
+                             // 568 -> 504-506 ms per step, same tokens (profiles/ab_r06_c5_plan*.txt).  Below 512 rows
+                             // the 4-wave 64-row groups stay (tools/dec_gemm_bench at 384 rows, profiles/dgb_r06_*).
+  int dec_big_fc2_kr = 1280; // ... fc2's K range per block on that plan (0: the whole K; 1280: four ranges, 240 blocks,
+                             // slabs summed by its residual + LayerNorm combine; whole K = 60 blocks, 50 us in the step)
   int dec_ln_fold = 0;       // ring passes (33..1024 rows): LayerNorms folded into their consumers (no combine launch
                              // after out / cout; fc2's combine writes stats instead of the LayerNorm).  Off: the
                              // consumers' epilogue costs more than the two launches it removes (dec_gemm 336 vs 319
@@ -609,15 +611,31 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     int cols = big ? ((tr >= 512 || !sq) ? 64 : 32) : e->dec_cols[proj];
     int lds = big ? (sq ? 144 : e->dec_big_lds) : 0;
     int waves = 4;
+    int kr_big = 0;
     if (b128) {                            // the 8-wave plan (dec_big128)
-      waves = 8;
-      if (sq) { p = 64; cols = 64; lds = 144; }
-      else if (proj == DEC_QKV) { p = 128; cols = 64; lds = 72; }
-      else { p = 128; cols = 128; lds = 144; }
+      if (sq) { p = 64; cols = 64; lds = 144; waves = 8; }
+      else { p = 128; cols = 128; lds = 144; waves = 8; }
+      // fc2 (K = 4d) in K ranges of dec_big_fc2_kr: as 128 x 128 tiles over the whole K (60 blocks) it took 50 us per
+      // launch in the step against 27.5 for the 4-wave 64 x 64 tiles (rocprof, config 5), though 25 us in
+      // tools/dec_gemm_bench: a block streams its 1.3 MB activation panel from the MALL at the per-CU rate, so few
+      // blocks lose in the step.  Qkv 128 x 64 (two blocks per CU) / fc1 128 x 64 / fc2 128 x 64 in two K ranges
+      // measured 5 / 2 / 10 ms per step slower (profiles/ab_r06_c5_plan2.txt)
+      if (proj == DEC_FC2) kr_big = e->dec_big_fc2_kr;
+      // VLOG_AMD_DEC_BIG_<QKV|SQ|FC1|FC2>="rows,cols,lds,kr,waves" overrides a projection's plan (A/B only)
+      static const int* const ov = [] {
+        static int v[4][5] = {};
+        const char* names[4] = {"VLOG_AMD_DEC_BIG_QKV", "VLOG_AMD_DEC_BIG_SQ", "VLOG_AMD_DEC_BIG_FC1", "VLOG_AMD_DEC_BIG_FC2"};
+        for (int i = 0; i < 4; ++i)
+          if (const char* e = std::getenv(names[i]))
+            if (std::sscanf(e, "%d,%d,%d,%d,%d", &v[i][0], &v[i][1], &v[i][2], &v[i][3], &v[i][4]) != 5) v[i][0] = 0;
+        return &v[0][0];
+      }();
+      const int* o = ov + 5 * (sq ? 1 : proj == DEC_QKV ? 0 : proj == DEC_FC1 ? 2 : 3);
+      if (o[0] > 0) { p = o[0]; cols = o[1]; lds = o[2]; kr_big = o[3]; waves = o[4]; }
     }
     if (p == -2 && launch_dec_oneshot(a, w, ldw, rows, N, K, ep, ws, wsb, N >= 3 * K ? 4 : 2, st)) return;
     // ring: one pass over each 1280-deep K range, epilogue in place (K > 1280: slabs summed by the combine)
-    const int kr = e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 || big ? K : 1280);
+    const int kr = kr_big > 0 ? std::min(kr_big, K) : e->dec_kr[proj] > 0 ? std::min(e->dec_kr[proj], K) : (K <= 1280 || big ? K : 1280);
     if (p > 0 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, kr, st, p, cols, lds, waves)) return;
     if (p == 0 && e->dec_ring && K <= 1280 && sl.total_rows <= 160 && launch_dec_ring(a, w, ldw, rows, N, K, ep, ws, wsb, 0, st))
       return;
@@ -664,7 +682,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     const int p = plan_of(proj);
     return p > 0 || (p == 0 && e->dec_ring && K <= 1280 && trows <= 160);
   };
-  const bool fold = e->dec_ln_fold && e->fold_ready && !ln_fuse && trows > 32 && trows <= 1024 && !(attn && align_map) &&
+  const bool b128_route = big_route && e->dec_big128 > 0 && trows >= e->dec_big128;   // 8-wave tiles take no fold
+  const bool fold = e->dec_ln_fold && e->fold_ready && !ln_fuse && trows > 32 && trows <= 1024 && !(attn && align_map) && !b128_route &&
                     ring_route(DEC_QKV, d) && ring_route(DEC_OUT, d) && ring_route(DEC_CQ, d) && ring_route(DEC_COUT, d) &&
                     ring_route(DEC_FC1, d) && ring_route(DEC_FC2, 4 * d) && e->dec_kr[DEC_QKV] == 0 &&
                     e->dec_kr[DEC_CQ] == 0 && e->dec_kr[DEC_FC1] == 0 && d % 16 == 0;
@@ -2671,6 +2690,10 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_mfma_fuse") e->cross_mfma_fuse = value ? 1 : 0;
     else if (k == "decode_gemm_big_rows") e->dec_big_rows = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
     else if (k == "decode_gemm_big128") e->dec_big128 = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
+    else if (k == "decode_gemm_big_fc2_kr") {
+      if (value != 0 && (value < 64 || value % 64 != 0)) throw std::runtime_error("decode_gemm_big_fc2_kr: 0 or a multiple of 64");
+      e->dec_big_fc2_kr = (int)std::min<int64_t>(value, 1 << 20);
+    }
     else if (k == "decode_ln_fold") e->dec_ln_fold = value ? 1 : 0;
     else if (k == "decode_gemm_big_lds") {
       if (value != 72 && value != 144) throw std::runtime_error("decode_gemm_big_lds: 72 or 144");
@@ -2722,6 +2745,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_mfma_fuse") *value = e->cross_mfma_fuse;
     else if (k == "decode_gemm_big_rows") *value = e->dec_big_rows;
     else if (k == "decode_gemm_big128") *value = e->dec_big128;
+    else if (k == "decode_gemm_big_fc2_kr") *value = e->dec_big_fc2_kr;
     else if (k == "decode_ln_fold") *value = e->dec_ln_fold;
     else if (k == "decode_gemm_big_lds") *value = e->dec_big_lds;
     else throw std::runtime_error("wm_get_option: unknown option " + k);
