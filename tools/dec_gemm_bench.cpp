@@ -15,7 +15,6 @@
 #include <vector>
 #include "../vlog_amd/csrc/gemm.h"
 
-void dec_lc_set_wblk(bool on);
 void launch_dec_gemm_body(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, float* ws, int KR, int abl,
                           hipStream_t st);
 
@@ -95,8 +94,6 @@ int main(int argc, char** argv) {
   const int ACOPY = std::getenv("DGB_ACOPIES") ? std::max(1, std::atoi(std::getenv("DGB_ACOPIES"))) : 1;
   CK(hipMalloc(&dA, maxA * 2 * ACOPY));
   CK(hipMalloc(&dW, maxW * 2 * NCOPY));
-  bf16* dWb = nullptr;                   // panel-blocked W copies (DGB_LC)
-  if (std::getenv("DGB_LC")) CK(hipMalloc(&dWb, maxW * 2 * NCOPY));
   CK(hipMalloc(&dC, maxC * 4));
   CK(hipMalloc(&dRef, maxC * 4));
   CK(hipMalloc(&ws, wsb));
@@ -159,60 +156,6 @@ int main(int argc, char** argv) {
         launch_gemm(a, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, st);
       });
       std::printf("%s N=%5d K=%5d  launch_gemm        %7.2f us  %7.1f GB/s(W)\n", s.name, s.N, s.K, us, wbytes / us / 1e3);
-    }
-    if (std::getenv("DGB_LC")) {
-      // the loader/consumer ring (gemm_lc.hip): block tile x K range
-      struct LcCfg { int bm, bn, kr; };
-      const LcCfg lcs[] = {{128, 128, 0}, {128, 64, 0}, {64, 128, 0}, {64, 64, 0}, {96, 32, 0}, {160, 32, 0},
-                           {160, 64, 0}, {64, 32, 0}, {32, 64, 0}, {32, 32, 0}, {128, 128, 1280}, {128, 64, 1280},
-                           {64, 64, 1280}, {128, 128, 2560}};
-      for (const auto& c : lcs) {
-        const int kr = c.kr >= s.K ? 0 : c.kr;
-        if (c.kr && !kr) continue;
-        CK(hipMemsetAsync(dC, 0, cbytes, st));
-        if (!launch_dec_lc(a, dW, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, c.bm, c.bn)) {
-          std::printf("%s lc %dx%d kr=%d unsupported\n", s.name, c.bm, c.bn, kr);
-          continue;
-        }
-        CK(hipStreamSynchronize(st));
-        const double err = f32 ? 0.0 : maxdiff();
-        const double us = timeit([&](int r) {
-          GemmA ar = a;
-          ar.ptr = dA + maxA * (r % ACOPY);
-          launch_dec_lc(ar, dW + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, c.bm, c.bn);
-        });
-        std::printf("%s N=%5d K=%5d  LC   bm=%3d bn=%3d kr=%4d          %7.2f us  %7.1f TF/s  rel diff %.1e\n", s.name, s.N,
-                    s.K, c.bm, c.bn, kr, us, 2.0 * M * s.N * s.K / us / 1e6, err);
-      }
-      // the same with W panel-blocked [N/BN][K/64][BN][64] (one contiguous run per column tile and K-step)
-      for (int bn : {128, 64}) {
-        if (s.N % bn) continue;
-        std::vector<uint16_t> hb((size_t)s.N * s.K);
-        for (int n = 0; n < s.N; ++n)
-          for (int k = 0; k < s.K; ++k)
-            hb[(((size_t)(n / bn) * (s.K / 64) + k / 64) * bn + (n % bn)) * 64 + (k % 64)] = hW[(size_t)n * s.K + k];
-        for (int c2 = 0; c2 < NCOPY; ++c2) CK(hipMemcpy(dWb + maxW * c2, hb.data(), (size_t)s.N * s.K * 2, hipMemcpyHostToDevice));
-        dec_lc_set_wblk(true);
-        for (int bm : {128, 64}) {
-          for (int krb : {0, 1280}) {
-            const int kr = krb >= s.K ? 0 : krb;
-            if (krb && !kr) continue;
-            CK(hipMemsetAsync(dC, 0, cbytes, st));
-            if (!launch_dec_lc(a, dWb, s.K, M, s.N, s.K, ep, ws, wsb, kr, st, bm, bn)) continue;
-            CK(hipStreamSynchronize(st));
-            const double err = f32 ? 0.0 : maxdiff();
-            const double us = timeit([&](int r) {
-              GemmA ar = a;
-              ar.ptr = dA + maxA * (r % ACOPY);
-              launch_dec_lc(ar, dWb + maxW * (r % NCOPY), s.K, M, s.N, s.K, ep, ws, wsb, kr, st, bm, bn);
-            });
-            std::printf("%s N=%5d K=%5d  LCWB bm=%3d bn=%3d kr=%4d          %7.2f us  %7.1f TF/s  rel diff %.1e\n", s.name,
-                        s.N, s.K, bm, bn, kr, us, 2.0 * M * s.N * s.K / us / 1e6, err);
-          }
-        }
-        dec_lc_set_wblk(false);
-      }
-      if (!big_only) continue;
     }
     if (big_only) {
       struct BigCfg { int rpb, cols, lds, kr, waves; };

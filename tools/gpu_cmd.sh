@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-VLOG_AMD_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > gpurun_out/bench_r06_rehearsal_2ranks.json 2> gpurun_out/bench_r06_rehearsal_2ranks.err || { tail -30 gpurun_out/bench_r06_rehearsal_2ranks.err; exit 1; }
-python3 -c "
-import json; d=json.load(open('gpurun_out/bench_r06_rehearsal_2ranks.json')); print(d['value'], d['n_gpus'], d['ranks'], d['config'].get('gpus_shared'), d.get('parity',{}).get('identical'))"
-grep -ci "nccl\|rccl" gpurun_out/bench_r06_rehearsal_2ranks.err || true
+DGB_LC=1 DGB_COPIES=40 DGB_ACOPIES=8 timeout -k 10 150 ./tools/dec_gemm_bench 50 750 > gpurun_out/dgb_r6_lcwb_750.txt 2>&1 || { tail -20 gpurun_out/dgb_r6_lcwb_750.txt; exit 1; }
+grep -E "LCWB|LC   bm=128 bn=128|LC   bm= 64 bn= 64" gpurun_out/dgb_r6_lcwb_750.txt | sed -E 's/ +/ /g'
+DGB_LC=1 DGB_COPIES=40 DGB_ACOPIES=8 timeout -k 10 150 ./tools/dec_gemm_bench 50 150 > gpurun_out/dgb_r6_lcwb_150.txt 2>&1 || { tail -20 gpurun_out/dgb_r6_lcwb_150.txt; exit 1; }
+grep -E "LCWB|LC   bm= 64 bn= 64|LC   bm= 96" gpurun_out/dgb_r6_lcwb_150.txt | sed -E 's/ +/ /g'

@@ -98,11 +98,6 @@ void launch_splitk_combine(const float* part, int splitk, int M, int N, const Ge
 bool launch_dec_ring(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
                      size_t ws_bytes, int kr, hipStream_t st, int rows_per_block = 0, int cols = 32, int lds_kb = 0,
                      int waves = 4);
-// Loader/consumer ring path (gemm_lc.hip): bm x bn per 512-thread block (4 loader waves streaming the operand panels
-// by LDS-DMA, 4 consumer waves running the MFMAs; per-slot counters in LDS instead of barriers), K range kr (0 =
-// whole K; slabs summed by launch_splitk_combine).  Bit-identical to launch_dec_ring for the same K range.
-bool launch_dec_lc(const GemmA& a, const bf16* w, long long ldw, int M, int N, int K, const GemmEpi& epi, float* ws,
-                   size_t ws_bytes, int kr, hipStream_t st, int bm, int bn);
 // Folded-LayerNorm vectors of a consumer projection (gemm_dec.hip): s = W g, c = W b + bias (f64 sums, f32 out).
 void launch_fold_vectors(const bf16* w, int N, int K, const float* g, const float* b, const float* bias, float* s_out,
                          float* c_out, hipStream_t st);
