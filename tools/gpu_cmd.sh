@@ -1,6 +1,14 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-DGB_LC=1 DGB_COPIES=40 DGB_ACOPIES=8 timeout -k 10 150 ./tools/dec_gemm_bench 50 750 > gpurun_out/dgb_r6_lcwb_750.txt 2>&1 || { tail -20 gpurun_out/dgb_r6_lcwb_750.txt; exit 1; }
-grep -E "LCWB|LC   bm=128 bn=128|LC   bm= 64 bn= 64" gpurun_out/dgb_r6_lcwb_750.txt | sed -E 's/ +/ /g'
-DGB_LC=1 DGB_COPIES=40 DGB_ACOPIES=8 timeout -k 10 150 ./tools/dec_gemm_bench 50 150 > gpurun_out/dgb_r6_lcwb_150.txt 2>&1 || { tail -20 gpurun_out/dgb_r6_lcwb_150.txt; exit 1; }
-grep -E "LCWB|LC   bm= 64 bn= 64|LC   bm= 96" gpurun_out/dgb_r6_lcwb_150.txt | sed -E 's/ +/ /g'
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_r06.log 2>&1 || { tail -20 gpurun_out/smoke_r06.log; exit 1; }
+tail -2 gpurun_out/smoke_r06.log
+VLOG_AMD_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > gpurun_out/bench_r06_rehearsal_2ranks.json 2> gpurun_out/bench_r06_rehearsal_2ranks.err || { tail -30 gpurun_out/bench_r06_rehearsal_2ranks.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/bench_r06_rehearsal_2ranks.json')); print(d['value'], d['n_gpus'], d['ranks'], d['config'].get('gpus_shared'), d.get('parity',{}).get('identical'))"
+echo "rccl/nccl mentions in rank logs: $(grep -ci 'nccl\|rccl' gpurun_out/bench_r06_rehearsal_2ranks.err || true)"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_r06 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-variable > $R/gpurun_out/prof_r06.log 2>&1 || { tail -30 $R/gpurun_out/prof_r06.log; exit 1; }
+head -12 $(ls $R/gpurun_out/prof_r06/*kernel_stats.csv | head -1) | cut -d, -f1-5
+tail -1 $R/gpurun_out/prof_r06.log
+BENCH_ARGS=--no-variable bash $R/tools/pmc_traffic.sh
