@@ -626,8 +626,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
         static int v[4][5] = {};
         const char* names[4] = {"VLOG_AMD_DEC_BIG_QKV", "VLOG_AMD_DEC_BIG_SQ", "VLOG_AMD_DEC_BIG_FC1", "VLOG_AMD_DEC_BIG_FC2"};
         for (int i = 0; i < 4; ++i)
-          if (const char* e = std::getenv(names[i]))
-            if (std::sscanf(e, "%d,%d,%d,%d,%d", &v[i][0], &v[i][1], &v[i][2], &v[i][3], &v[i][4]) != 5) v[i][0] = 0;
+          if (const char* ev = std::getenv(names[i]))
+            if (std::sscanf(ev, "%d,%d,%d,%d,%d", &v[i][0], &v[i][1], &v[i][2], &v[i][3], &v[i][4]) != 5) v[i][0] = 0;
         return &v[0][0];
       }();
       const int* o = ov + 5 * (sq ? 1 : proj == DEC_QKV ? 0 : proj == DEC_FC1 ? 2 : 3);
