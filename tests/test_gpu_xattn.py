@@ -214,3 +214,44 @@ def test_large_v3_factored_matches_projected():
     assert sum(len(r.tokens) for r in rb) > W * 5
     eng.set_option("cross_mode", 1)
     assert eng.device_bytes() > 0
+
+
+def test_large_v3_dma_form_bit_identical():
+    """The LDS-DMA form of the factored attention (the default at d = 1280, option cross_attn_dma) against the
+    register-staged form: the same work items, per-wave MFMAs and fixed-order cross-wave sums, so the same bits --
+    teacher-forced logits over a 40-row prompt (two m-tiles per window), alignment-head capture on the attention
+    kernel (cross_tf 0), greedy and beam-5 decodes (1 and 5 rows per window, rows finishing at different steps)."""
+    W = 4
+    dims, sd, eng, enc = _engine("large-v3", 2, W, eot_after=30)
+    del sd
+    st = dims.specials
+    heads = dims.default_alignment_heads()
+    toks = np.array([[st.sot, st.lang_token("en"), st.transcribe, st.no_timestamps] + list(range(500 + 40 * i, 536 + 40 * i))
+                     for i in range(2)])
+    prompt = [st.sot, st.lang_token("en"), st.transcribe]
+    assert eng.option("cross_attn_dma") == 1
+    out = {}
+    try:
+        for form in (0, 1):
+            eng.set_option("cross_attn_dma", form)
+            eng.set_option("cross_tf", 0)
+            eng.reserve(W, 5 * W)
+            eng.cross_kv(enc, 0)
+            lg, at = eng.forward([3, 1], toks, align_heads=heads)
+            eng.set_option("cross_tf", 1)
+            g, _ = eng.generate(list(range(W)), [prompt] * W, suppress_tokens=_sup(st), max_length=60)
+            b, _ = eng.generate(list(range(W)), [prompt] * W, beam_size=5, patience=1.0, suppress_tokens=_sup(st),
+                                max_length=60)
+            out[form] = (lg.cpu().numpy(), at.cpu().numpy(), g, b)
+    finally:
+        eng.set_option("cross_attn_dma", 1)
+        eng.set_option("cross_tf", 1)
+    (la, aa, ga, ba), (lb, ab, gb, bb) = out[0], out[1]
+    assert np.all(np.isfinite(lb)) and np.allclose(ab.sum(-1), 1.0, atol=1e-4)
+    assert np.array_equal(la, lb), np.abs(la - lb).max()
+    assert np.array_equal(aa, ab), np.abs(aa - ab).max()
+    for ra, rb in ((ga, gb), (ba, bb)):
+        assert [r.tokens for r in ra] == [r.tokens for r in rb]
+        assert [r.score for r in ra] == [r.score for r in rb]
+        assert [r.no_speech_prob for r in ra] == [r.no_speech_prob for r in rb]
+    assert sum(len(r.tokens) for r in gb) > W * 5

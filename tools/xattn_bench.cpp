@@ -9,7 +9,7 @@
 #include <vector>
 typedef __bf16 bf16;
 void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int,
-                  int, int, int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t,
+                  int, int, int, int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t,
                   hipEvent_t);
 void xattn_set_ablation(int);
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
@@ -56,6 +56,7 @@ int main(int argc, char** argv) {
   const int snake = getenv("XB_SNAKE") ? atoi(getenv("XB_SNAKE")) : 0;
   int launch_no = 0;
   const int keep = getenv("XB_KEEP") ? atoi(getenv("XB_KEEP")) : 0;   // windows loaded with the default policy
+  const int dma = getenv("XB_DMA") ? atoi(getenv("XB_DMA")) : 1;      // bf16: 1 = LDS-DMA form, 0 = register-staged
   for (int f8 = 0; f8 < 2; ++f8) {
     if (f8_only >= 0 && f8 != f8_only) continue;
     const double bytes = (double)W * T * d * (f8 ? 1 : 2);
@@ -63,7 +64,7 @@ int main(int argc, char** argv) {
       xattn_set_ablation(abl);
       for (int splits : split_list) {
         auto run = [&] {
-          launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, splits, snake ? (launch_no++ & 1) : 0, keep, pu, pml, nullptr,
+          launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, splits, snake ? (launch_no++ & 1) : 0, keep, dma, pu, pml, nullptr,
                        nullptr, 0, nullptr, 0, nullptr, nullptr);
         };
         for (int i = 0; i < 3; ++i) run();
@@ -74,7 +75,8 @@ int main(int argc, char** argv) {
         float ms = 0;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = 1000.0 * ms / iters;
-        printf("%s%s abl %2d splits %2d  %8.2f us  %7.1f GB/s (encoder output)\n", f8 ? "fp8 " : "bf16", snake ? " snake" : "", abl, splits, us,
+        printf("%s%s%s abl %2d splits %2d  %8.2f us  %7.1f GB/s (encoder output)\n", f8 ? "fp8 " : "bf16", !f8 && dma ? " dma" : "",
+               snake ? " snake" : "", abl, splits, us,
                bytes / (us * 1e-6) / 1e9);
       }
     }

@@ -41,6 +41,7 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #define XTHR 8.0f              // deferred-rescale threshold (log2 units)
 #define XMAXS 16               // max key splits
@@ -518,6 +519,299 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------------
+// LDS-DMA form (bf16 cross memory, d = 1280: 8 waves x 160 columns; the default there).  The same work items, the
+// same per-wave MFMAs and the same fixed-order cross-wave sum as xattn_segment, so the same bits; what changes is
+// how E reaches LDS and where the S partials live:
+//   - each wave streams its 10 KB slice of a tile straight into LDS (10 global_load_lds_dwordx4 of 1 KiB; the
+//     image's chunk swizzle goes on the per-lane SOURCE address), two tiles ahead, into a ring of two 80 KB slots
+//     that fills the whole 160 KB LDS -- no staging registers, no ds_write of E;
+//   - after a wave has read its slice of the current tile (the S operand, and the U operand of rows 0-15), that part
+//     of the slice is dead, and the S partials (4 KB) and their sums (512 B) are written there;
+//   - a third barrier per tile (after every wave has read the sums) frees the slot, and each wave then issues its
+//     DMAs of tile + 2 into it: a tile's loads are in flight for about one and a half tiles of compute.
+// Waits are counted vmcnt + raw s_barrier (no barrier drains the DMA queue: MI355X_MICROARCH.md item 7); q' is
+// loaded by inline asm and waited for explicitly, because the compiler waits vmcnt(0) at the first use of an
+// ordinary load's result while LDS-DMA is in flight (cdna_hip_programming.md §5, "Pipelining across barriers").
+#define XD_QW 160
+#define XD_NW 8
+#define XD_IMG (32 * XD_QW * 2)            // bytes of one wave's slice of a tile
+#define XD_LS (XD_IMG / 1024)              // its LDS-DMA instructions
+#define XD_SLOT (XD_NW * XD_IMG)
+
+template <bool NT, int ABL, bool CAP>
+__device__ __forceinline__ void xattn_segment_dma(const XAttnArgs& a, char* smem, int grp, int mt, int split, int tb,
+                                                  int te) {
+  constexpr int QW = XD_QW, NW = XD_NW, KS = QW / 16, CT = QW / 32, LDR = xldr(QW), CPR = QW / 8, IMG = XD_IMG,
+                LS = XD_LS, SLOT = XD_SLOT;
+  static_assert(LDR == QW && IMG % 1024 == 0, "unpadded image rows, whole DMA instructions");
+  static_assert(16 * 64 * 4 + 64 * 8 <= 16 * LDR * 2, "the S partials and sums fit in rows 0-15 of the slice");
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int M = a.G * a.H;
+  const int m = mt * 32 + l32;
+  const int row0 = grp * a.G;
+  int row = row0, hd = 0;
+  bool valid = m < M;
+  if (valid) {
+    const int ri = m / a.H;
+    row = row0 + ri;
+    hd = m - ri * a.H;
+    valid = !(a.done && a.done[a.row_hyp[row]]);
+  }
+  if (!__any(valid)) return;             // identical in all waves: uniform exit before any barrier
+  const int slot = a.hyp_slot[a.row_hyp[row0]];
+  const int cb = wv * QW;
+  const int n_tiles = (a.T + 31) / 32;
+  const char* EB16 = (const char*)a.enc + ((long long)slot * n_tiles * NW + wv) * (long long)IMG;
+  {
+    const unsigned long long nq = __popcll(__ballot(valid && hh == 0));
+    if (a.stat && tid == 0) {
+      const long long npos = (long long)min(te * 32, a.T) - tb * 32;
+      unsigned long long by = nq * (unsigned long long)a.d * 2;
+      if (mt == 0) by += (unsigned long long)(npos * a.d * 2);
+      atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), by);
+    }
+  }
+  bf16x8 qf[KS];
+  {
+    const bf16* qr = a.qp + ((long long)row * a.H + hd) * a.d + cb + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = *(const bf16x8*)(qr + 16 * s);     // unconditional: row, hd are clamped
+  }
+  // DMA i of a tile fills LDS bytes [1024 i, 1024 i + 1024) of the wave's slice: lane l writes image granule
+  // p = 64 i + l = (row r, slot s), which holds chunk c = s ^ ((r >> 2) & 3) of row r (xchunk is an involution)
+  int goff[LS];
+#pragma unroll
+  for (int i = 0; i < LS; ++i) {
+    const int p = 64 * i + lane, r = p / CPR, s = p - r * CPR;
+    goff[i] = (r * CPR + xchunk(r, s)) * 16;
+  }
+  auto issue = [&](int tile) {
+    const char* src = EB16 + (long long)tile * SLOT;
+    char* dst = smem + (tile & 1) * SLOT + wv * IMG;
+#pragma unroll
+    for (int i = 0; i < LS; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src + goff[i]), (__attribute__((address_space(3))) void*)(dst + 1024 * i),
+                                       16, 0, NT ? 2 : 0);
+  };
+  if constexpr ((ABL & 16) != 0) {       // compute-only ablation: finite constant images instead of loads
+#pragma unroll
+    for (int i = 0; i < 2 * LS; ++i)
+      *(i32x4*)(smem + (i / LS) * SLOT + wv * IMG + 1024 * (i % LS) + 16 * lane) = i32x4{0x3c003c00, 0x3c003c00, 0x3c003c00, 0x3c003c00};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  } else {
+    issue(tb);
+  }
+  // A use of q' here: the compiler waits vmcnt(0) for it -- q' and the first tile, which the first tile needs anyway --
+  // and no later use waits.  Only then the second tile's DMAs (a whole tile of compute ahead of their use).
+  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]), "v"(qf[4]), "v"(qf[5]), "v"(qf[6]), "v"(qf[7]),
+               "v"(qf[8]), "v"(qf[9]));
+  static_assert(KS == 10 && LS == 10, "10 q' fragments; the vmcnt immediates count 10 DMAs per tile");
+  if constexpr ((ABL & 16) == 0) {
+    if (tb + 1 < te) issue(tb + 1);
+  }
+  if (!valid) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = bf16x8{};
+  }
+  f32x16 o[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) o[c] = xzero16();
+  float m_run = -INFINITY, l_run = 0.f;
+  float* pr_row = nullptr;
+  if (a.probs && wv == 0 && valid) {
+    const int hm = a.head_map[hd];
+    if (hm >= 0) pr_row = a.probs + ((long long)row * a.n_align + hm) * a.T;
+  }
+  for (int tile = tb; tile < te; ++tile) {
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    char* base = smem + (tile & 1) * SLOT;
+    bf16* sE = (bf16*)(base + wv * IMG);
+    bf16* sER = sE + 16 * LDR;
+    if constexpr ((ABL & 16) == 0) {     // this wave's DMAs of the tile have landed (those of tile + 1 may not)
+      if (tile + 1 < te) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    f32x16 sc = xzero16();
+    // transposed U operand reads (see xattn_segment): rows 16 ks .. 16 ks + 15
+    const int G4 = (lo >> 4) & 3, gi = lo & 15, gq = gi >> 2, gp = gi & 3;
+    const int lowc = 2 * (G4 & 1) + (gp >> 1);
+    const int o0 = (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
+    const int o1 = (8 + 4 * hh + gq) * LDR + 8 * (lowc ^ (2 + hh)) + 4 * (gp & 1);
+    // LDS reads and writes that the DMA's destination may alias are inline asm: the compiler gives the tr16 intrinsic
+    // no alias information and cannot tell the other accesses from the DMA's destination, and would wait vmcnt(0) --
+    // drain the DMA of tile + 1 -- before them.  Each asm block that loads waits for its own loads (lgkmcnt(0)) and
+    // marks its outputs early-clobber: an asm output that returns after the statement could be copied by the compiler
+    // before it arrives.
+    auto lds_addr = [](const bf16* p) -> unsigned {
+      return (unsigned)(size_t)(__attribute__((address_space(3))) const bf16*)p;
+    };
+    // the 5 column tiles' transposed fragments of one 16-row half image (two ds_read_b64_tr_b16 each, 64 B apart per c)
+    auto ufrags = [&](const bf16* img, bf16x8 (&u)[CT]) {
+      static_assert(CT == 5, "the U fragment reads list 5 column tiles");
+      xi32x2 v[10];
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %10\n\tds_read_b64_tr_b16 %1, %11\n\t"
+          "ds_read_b64_tr_b16 %2, %10 offset:64\n\tds_read_b64_tr_b16 %3, %11 offset:64\n\t"
+          "ds_read_b64_tr_b16 %4, %10 offset:128\n\tds_read_b64_tr_b16 %5, %11 offset:128\n\t"
+          "ds_read_b64_tr_b16 %6, %10 offset:192\n\tds_read_b64_tr_b16 %7, %11 offset:192\n\t"
+          "ds_read_b64_tr_b16 %8, %10 offset:256\n\tds_read_b64_tr_b16 %9, %11 offset:256\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
+            "=&v"(v[8]), "=&v"(v[9])
+          : "v"(lds_addr(img + o0)), "v"(lds_addr(img + o1))
+          : "memory");
+#pragma unroll
+      for (int c = 0; c < CT; ++c) u[c] = __builtin_bit_cast(bf16x8, i32x4{v[2 * c][0], v[2 * c][1], v[2 * c + 1][0], v[2 * c + 1][1]});
+    };
+    bf16x8 u0[CT];
+    if constexpr ((ABL & 7) != 7) {
+      const int l32o = lo & 31, g = (l32o >> 2) & 3;
+      const bf16* rb = l32o < 16 ? sE + l32o * LDR : sER + (l32o - 16) * LDR;
+      const bf16* s0 = rb + 8 * (hh ^ g);
+      const bf16* s1 = rb + 8 * ((2 + hh) ^ g);
+      bf16x8 ea[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) ea[s] = *(const bf16x8*)(((s & 1) ? s1 : s0) + 32 * (s >> 1));
+      ufrags(sE, u0);                                          // rows 0-15: their bytes are reused below
+#pragma unroll
+      for (int s = 0; s < KS; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ea[s], qf[s], sc, 0, 0, 0);
+      // the partials into the dead rows 0-15 of this wave's slice (LDS is in order: after the reads above).  Stores as
+      // inline asm too: the compiler cannot tell them from the DMA's destination and would wait vmcnt(0) first.
+      const unsigned px = lds_addr(sE) + 8 * lane;
+      // the compiler's hazard recognizer does not look into inline asm: the wait states between the last S MFMA
+      // writing sc and the first store reading it (a 16-pass MFMA's result read by a non-MFMA: 18) are spelled out
+      asm volatile("s_nop 15\n\ts_nop 3" : "+v"(sc)::"memory");
+#define XD_W2(k_) asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(px), "v"(float2{sc[2 * k_], sc[2 * k_ + 1]}), "i"(512 * k_) : "memory")
+      XD_W2(0); XD_W2(1); XD_W2(2); XD_W2(3); XD_W2(4); XD_W2(5); XD_W2(6); XD_W2(7);
+#undef XD_W2
+      xbarrier<true>();
+      // wave w sums registers 2w, 2w + 1 over the waves in order 0..7 (xattn_segment's order); reads as asm as well
+      static_assert(NW == 8 && IMG * 3 + 4096 + 512 <= 65536, "4 slices within one 16-bit LDS offset");
+      // the 8 waves' float2 at byte offset `off` of their slices (slices 0-3 from pr, 4-7 from pr + 4 IMG), waited
+      auto read8 = [&](unsigned pr, auto offc, float2 (&t)[NW]) {
+        constexpr int off = decltype(offc)::value;
+        asm volatile(
+            "ds_read_b64 %0, %8 offset:%10\n\tds_read_b64 %1, %8 offset:%11\n\t"
+            "ds_read_b64 %2, %8 offset:%12\n\tds_read_b64 %3, %8 offset:%13\n\t"
+            "ds_read_b64 %4, %9 offset:%10\n\tds_read_b64 %5, %9 offset:%11\n\t"
+            "ds_read_b64 %6, %9 offset:%12\n\tds_read_b64 %7, %9 offset:%13\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7])
+            : "v"(pr), "v"(pr + 4 * IMG), "i"(off), "i"(off + IMG), "i"(off + 2 * IMG), "i"(off + 3 * IMG)
+            : "memory");
+      };
+      float2 t[NW];
+      {
+        read8(lds_addr((const bf16*)base) + 8 * (wv * 64 + lane), std::integral_constant<int, 0>{}, t);
+        float2 v = t[0];
+#pragma unroll
+        for (int w2 = 1; w2 < NW; ++w2) {
+          v.x += t[w2].x;
+          v.y += t[w2].y;
+        }
+        asm volatile("ds_write_b64 %0, %1 offset:4096" ::"v"(px), "v"(v) : "memory");
+      }
+      xbarrier<true>();
+      {
+        read8(lds_addr((const bf16*)base) + 8 * lane, std::integral_constant<int, 4096>{}, t);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          sc[2 * k] = t[k].x;
+          sc[2 * k + 1] = t[k].y;
+        }
+      }
+    }
+    bf16x8 u1[CT];
+    if constexpr ((ABL & 7) != 7) {
+      ufrags(sER, u1);                                         // rows 16-31: untouched by the partials
+    }
+    const int t0 = tile * 32;
+    if (t0 + 32 > a.T) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (t0 + 8 * (r >> 2) + 4 * hh + (r & 3) >= a.T) sc[r] = -INFINITY;
+    }
+    if (CAP && pr_row) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = t0 + 8 * (r >> 2) + 4 * hh + (r & 3);
+        if (t < a.T) pr_row[t] = sc[r];
+      }
+    }
+    // every wave's reads of this slot are complete: its slices take tile + 2 (the CAP stores above are older than
+    // these DMAs, so the next tile's counted wait covers them)
+    if constexpr ((ABL & 7) != 7) xbarrier<true>();
+    if constexpr ((ABL & 16) == 0) {
+      if (tile + 2 < te) issue(tile + 2);
+    }
+    if constexpr ((ABL & 7) != 7) {
+      float mx = sc[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (__any(mx > m_run + XTHR)) {
+        const float mn = fmaxf(m_run, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+        l_run *= alpha;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+        m_run = mn;
+      }
+      bf16x8 pf[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(sc[r] - m_run);
+        l_run += p;
+        pf[r >> 3][r & 7] = f2bf(p);
+      }
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(u0[c], pf[0], o[c], 0, 0, 0);
+        o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(u1[c], pf[1], o[c], 0, 0, 0);
+      }
+    }
+  }
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (valid) {
+    const float inv = 1.0f / l_run;
+    const long long pi = ((long long)split * a.slab_rows + row) * a.H + hd;
+    if (wv == 0 && hh == 0) {
+      a.part_ml[2 * pi] = m_run;
+      a.part_ml[2 * pi + 1] = l_run;
+    }
+    const long long kstride = a.slab_rows * 16;
+    bf16* up = a.part_u + (((long long)split * a.H + hd) * (a.d / 16) + cb / 16) * kstride + (long long)row * 16 + 4 * hh;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[c][4 * g + e] * inv);
+        *(bf16x4*)(up + (2 * c + (g >> 1)) * kstride + 8 * (g & 1)) = w;
+      }
+  }
+}
+
+template <int ABL = 0, bool CAP = false>
+__global__ __launch_bounds__(XD_NW * 64) void xattn_dma_kernel(XAttnArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * XD_SLOT];
+  const int n_tiles = (a.T + 31) / 32;
+  const int j = blockIdx.x >> 3;
+  const int item = (blockIdx.x & 7) * a.per_xcd + (a.rev ? a.per_xcd - 1 - j : j);
+  if (item >= a.n_items) return;
+  const int mt = item % a.n_mt;
+  const int rest = item / a.n_mt;
+  const int split = rest % a.splits, grp = rest / a.splits;
+  const int tb = split * n_tiles / a.splits, te = (split + 1) * n_tiles / a.splits;
+  if (ABL == 0 && grp < a.keep) xattn_segment_dma<false, ABL, CAP>(a, smem, grp, mt, split, tb, te);
+  else xattn_segment_dma<true, ABL, CAP>(a, smem, grp, mt, split, tb, te);
+}
+
+// ------------------------------------------------------------------------------------------------------
 struct XCombArgs {
   const bf16* part_u; const float* part_ml; int splits; long long slab_rows;
   const bf16* wvb; const float* bv;      // this layer's V projection packed [H][d/16][64][16], bias [d]
@@ -808,7 +1102,8 @@ static int g_xattn_abl = [] {            // ablation / load-policy experiments (
 void xattn_set_ablation(int abl) { g_xattn_abl = abl; }
 
 void launch_xattn(const bf16* qp, const void* enc, const float* escale, const int* hyp_slot, const int* row_hyp,
-                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, int rev, int keep, bf16* part_u,
+                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, int rev, int keep,
+                  int dma, bf16* part_u,
                   float* part_ml, float* probs, const int* head_map, int n_align, unsigned long long* stat,
                   hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
@@ -830,8 +1125,18 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
 #define XA_LAUNCH_F(QW_, NW_, DP_, F8_)                                                                            \
   if (probs) { XA_LAUNCH_C(QW_, NW_, DP_, F8_, true) } else { XA_LAUNCH_C(QW_, NW_, DP_, F8_, false) }
 #define XA_LAUNCH(QW_, NW_, DP_) XA_LAUNCH_F(QW_, NW_, DP_, false)
+  const bool dma_form = dma && !escale && d == XD_NW * XD_QW;
   if (a.abl) {                           // microbenchmark ablations (tools/xattn_bench): d = 1280, default form only
     if (d != 1280) throw std::runtime_error("xattn: ablations are built for n_state 1280 only");
+    if (dma_form) {                      // LDS-DMA form: loads only (7) or compute only (16)
+      switch (a.abl) {
+        case 7: hipLaunchKernelGGL((xattn_dma_kernel<7>), grid, dim3(XD_NW * 64), 0, st, a); break;
+        case 16: hipLaunchKernelGGL((xattn_dma_kernel<16>), grid, dim3(XD_NW * 64), 0, st, a); break;
+        default: throw std::runtime_error("xattn: unsupported ablation of the LDS-DMA form");
+      }
+      WM_LAUNCH_CHECK("xattn_dma_kernel");
+      return;
+    }
 #define XA_ABL(F8_, AB_) \
     case AB_: hipLaunchKernelGGL((xattn_kernel<160, 8, 1, F8_, AB_>), grid, dim3(512), 0, st, a); break;
     if (escale) {
@@ -855,6 +1160,17 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
       default: throw std::runtime_error("xattn: unsupported n_state " + std::to_string(d));
     }
     WM_LAUNCH_CHECK("xattn_kernel");
+    return;
+  }
+  if (dma_form) {
+    if (probs) {
+      if (ev0) hipExtLaunchKernelGGL((xattn_dma_kernel<0, true>), grid, dim3(XD_NW * 64), 0, st, ev0, ev1, 0, a);
+      else hipLaunchKernelGGL((xattn_dma_kernel<0, true>), grid, dim3(XD_NW * 64), 0, st, a);
+    } else {
+      if (ev0) hipExtLaunchKernelGGL((xattn_dma_kernel<0, false>), grid, dim3(XD_NW * 64), 0, st, ev0, ev1, 0, a);
+      else hipLaunchKernelGGL((xattn_dma_kernel<0, false>), grid, dim3(XD_NW * 64), 0, st, a);
+    }
+    WM_LAUNCH_CHECK("xattn_dma_kernel");
     return;
   }
   // 8 waves x d/8 columns (4 x d/4 at d = 384), one tile staged ahead: 80 KB of E in flight per CU at d = 1280

@@ -51,7 +51,7 @@ void launch_xquant8(const bf16*, long long, int, unsigned char*, float*, hipStre
 long long xblock_slot_elems(int T, int d);
 void launch_xblock(const bf16* src, int B, int T, int d, bf16* dst, bool to_blocked, hipStream_t st);
 void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int, int, int,
-                  bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
+                  int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
 void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, const float*, const int*, const int*, bf16*,
                      long long, int, int, int, int, int, float*, const int*, int, hipStream_t);
 
@@ -248,6 +248,8 @@ struct wm_engine {
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
                              // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
+  int xdma = 1;              // factored cross-attention, bf16 at n_state 1280: 1 = the LDS-DMA form (default), 0 = the
+                             // register-staged form (same bits; attn_xenc.hip)
   DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs (cross_fp8: OCP e4m3 bytes)
   DevBuf xscale;             // cross_fp8: [n_slots][T] f32 per-position scales
   int cross_fp8 = 0;         // opt-in fp8 cross memory (factored form only; changes numerics, never the default)
@@ -798,7 +800,7 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     {
       ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
       launch_xattn(qp, e->xenc.p, e->cross_fp8 ? e->xscale.as<float>() : nullptr, e->d_hyp_slot.as<int>(), row_hyp, done, rows, sl.total_rows, cross_group, H, T,
-                   d, splits, e->xsnake ? (l & 1) : 0, e->xkeep, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+                   d, splits, e->xsnake ? (l & 1) : 0, e->xkeep, e->xdma, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
     }
     {
       ProfScope ps(e, P_CROSS_COMB, st, 2.0 * rows * d * d, 2.0 * d * d + 2.0 * splits * rows * prow + 2.0 * rows * d);
@@ -2347,6 +2349,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_CROSS_MODE")) e->cross_mode = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_XSNAKE")) e->xsnake = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_XKEEP")) e->xkeep = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("VLOG_AMD_XDMA")) e->xdma = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_LDS")) e->dec_big_lds = std::atoi(v) == 144 ? 144 : 72;
     if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_ROWS")) e->dec_big_rows = std::max(0, std::atoi(v));
@@ -2654,6 +2657,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_attn_fuse") e->cross_fuse = (int)(value & 3);
     else if (k == "cross_attn_snake") e->xsnake = value != 0;
     else if (k == "cross_attn_keep") e->xkeep = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
+    else if (k == "cross_attn_dma") e->xdma = value != 0;
     else if (k == "gemm_persistent") gemm_8p_set_persistent((int)value);
     else if (k == "align_fused") align_set_fused((int)value);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
@@ -2733,6 +2737,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_attn_fuse") *value = e->cross_fuse;
     else if (k == "cross_attn_snake") *value = e->xsnake;
     else if (k == "cross_attn_keep") *value = e->xkeep;
+    else if (k == "cross_attn_dma") *value = e->xdma;
     else if (k == "gemm_persistent") *value = gemm_8p_get_persistent();
     else if (k == "align_fused") *value = align_get_fused();
     else if (k == "encode_chunk") *value = e->enc_chunk;
