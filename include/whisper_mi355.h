@@ -276,8 +276,12 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   measured no gain).  Bit-identical.
  *   "cross_attn_snake" (default 0): odd decoder layers walk the factored cross-attention's items in reverse, so
  *   the encoder output read last by one layer is read first by the next (Infinity Cache reuse).  Bit-identical.
- *   "cross_attn_dma" (default 1): at n_state 1280 with bf16 cross memory, the factored cross-attention streams the
- *   encoder output straight into LDS (LDS-DMA, two tiles ahead); 0 runs the register-staged form.  Bit-identical.
+ *   "cross_attn_dma" (default 0): 1 = at n_state 1280 with bf16 cross memory, the factored cross-attention streams the
+ *   encoder output straight into LDS (LDS-DMA, two tiles ahead); 0 runs the register-staged form.  Bit-identical on
+ *   key-split items; measured slower in the bench step.
+ *   "cross_attn_chunks" (default 1): with the LDS-DMA form, greedy passes cut their (window, 32-position tile) units into
+ *   one contiguous chunk per CU (stream-K) instead of per-window key splits; the pieces of a window are merged like
+ *   key splits, so results agree to f32 rounding, not bit for bit.  0 = key splits.
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its
  *   (window, head, key split) items with a grid stride; 0 launches one block per item.
  *   "cross_attn_fuse" (default 1): bit 0 folds the cq projection's split-K combine into the cross-attention

@@ -7,10 +7,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-typedef __bf16 bf16;
+#include "../vlog_amd/csrc/common.h"
 void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int,
-                  int, int, int, int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t,
-                  hipEvent_t);
+                  int, int, const XPlan&, int, int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*,
+                  hipStream_t, hipEvent_t, hipEvent_t);
+XPlan xattn_plan(int, int, int, int, int, bool);
 void xattn_set_ablation(int);
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -57,15 +58,18 @@ int main(int argc, char** argv) {
   int launch_no = 0;
   const int keep = getenv("XB_KEEP") ? atoi(getenv("XB_KEEP")) : 0;   // windows loaded with the default policy
   const int dma = getenv("XB_DMA") ? atoi(getenv("XB_DMA")) : 1;      // bf16: 1 = LDS-DMA form, 0 = register-staged
+  const int sk = getenv("XB_SK") ? atoi(getenv("XB_SK")) : 1;         // LDS-DMA form: 1 = stream-K chunks (ignores splits)
   for (int f8 = 0; f8 < 2; ++f8) {
     if (f8_only >= 0 && f8 != f8_only) continue;
     const double bytes = (double)W * T * d * (f8 ? 1 : 2);
     for (int abl : abls) {
       xattn_set_ablation(abl);
       for (int splits : split_list) {
+        XPlan plan = xattn_plan(W, 1, H, T, d, !f8 && dma && sk && !snake && !keep);
+        if (!plan.sk_W) plan.slabs = splits;
         auto run = [&] {
-          launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, splits, snake ? (launch_no++ & 1) : 0, keep, dma, pu, pml, nullptr,
-                       nullptr, 0, nullptr, 0, nullptr, nullptr);
+          launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, plan, snake ? (launch_no++ & 1) : 0, keep, dma, 0, pu, pml,
+                       nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr);
         };
         for (int i = 0; i < 3; ++i) run();
         CK(hipEventRecord(e0, 0));
@@ -75,8 +79,8 @@ int main(int argc, char** argv) {
         float ms = 0;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = 1000.0 * ms / iters;
-        printf("%s%s%s abl %2d splits %2d  %8.2f us  %7.1f GB/s (encoder output)\n", f8 ? "fp8 " : "bf16", !f8 && dma ? " dma" : "",
-               snake ? " snake" : "", abl, splits, us,
+        printf("%s%s%s abl %2d splits %2d  %8.2f us  %7.1f GB/s (encoder output)\n", f8 ? "fp8 " : "bf16",
+               plan.sk_W ? " dma chunks" : !f8 && dma ? " dma" : "", snake ? " snake" : "", abl, plan.sk_W ? plan.sk_P : splits, us,
                bytes / (us * 1e-6) / 1e9);
       }
     }

@@ -75,13 +75,16 @@ __device__ __forceinline__ void xbarrier() {
     __syncthreads();
   }
 }
+// swap bits 2 and 3 of a column's position in its 16-column block (the u record order: xstore_u)
+__host__ __device__ constexpr int xswap23(int x) { return (x & 3) | ((x >> 1) & 4) | ((x << 1) & 8); }
 __host__ __device__ constexpr int xldr(int qw) { return (qw / 8 + ((4 - qw / 8) % 16 + 16) % 16) * 8; }
 
 // ------------------------------------------------------------------------------------------------------
 // Weight packing, from the fused [L][K|V][d][d] cross projection (engine weight "dec.ckv.w"); runs once per
 // weight upload:
 //   wkt[l][h][c][j]            = Wk_l[h*64 + j][c]   (xq's A operand: 64 contiguous j per c)
-//   wvb[l][h][c/16][j][c%16]   = Wv_l[h*64 + j][c]   (xcomb's B operand: one k-step of 32 j = 1 KB contiguous)
+//   wvb[l][h][c/16][j][p]      = Wv_l[h*64 + j][16 (c/16) + xswap23(p)]   (xcomb's B operand: one k-step of 32 j = 1 KB
+//                                contiguous; within a 16-column block in the order xstore_u writes u)
 __global__ void xpack_kernel(const bf16* __restrict__ ckv_w, bf16* __restrict__ wkt, bf16* __restrict__ wvb, int L,
                              int H, int d) {
   const long long total = (long long)L * H * d * 64;
@@ -102,7 +105,7 @@ __global__ void xpack_kernel(const bf16* __restrict__ ckv_w, bf16* __restrict__ 
       const int kb = (int)(r2 % (d / 16));
       const long long lh = r2 / (d / 16);
       const int h = (int)(lh % H), l = (int)(lh / H);
-      wvb[idx] = ckv_w[((long long)l * 2 * d + d + h * 64 + j) * d + kb * 16 + c16];
+      wvb[idx] = ckv_w[((long long)l * 2 * d + d + h * 64 + j) * d + kb * 16 + xswap23(c16)];
     }
   }
 }
@@ -215,12 +218,34 @@ struct XAttnArgs {
   float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
   float* probs; const int* head_map; int n_align;   // capture: raw scores [row][n_align][T]
   unsigned long long* stat;
+  long long sk_W; int sk_P, sk_lane0, sk_lanes, sk_c0, sk_map;   // LDS-DMA chunks (stream-K): units of the whole pass, chunk count,
+                                         // this launch's first lane (of the pass) and lane count, its first chunk; sk_W = 0: items
   int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0, and the
                                          // product kernel is compiled without them: template ABL): bit 0 skips
                                          // the S MFMAs, bit 1 the cross-wave sum, bit 2 the U phase, bit 3
                                          // loads E with plain loads (same-box bench: 1 % slower than
                                          // non-temporal ones; tools/gpu_ablib.sh), bit 4 skips the E loads
 };
+
+// A split partial u / l of one (row, head) column as bf16 (up = its 16-element record in column block 0 of the wave's
+// columns; kstride = elements per column block).  Accumulator register 4 g + e of column tile c holds column
+// 32 c + 8 g + 4 hh + e (relative to the wave's first), i.e. 16-column block 2 c + (g >> 1) at column 8 (g & 1) + 4 hh + e.
+// The record stores position 8 hh + 4 (g & 1) + e (bits 2 and 3 of the column swapped, xswap23): each lane writes its
+// 8 values of a block as one 16-B store, so one store instruction covers 32 rows x 32 B = 1 KB contiguous (8-B pieces
+// half-filled every line per instruction).  xpack_kernel packs Wv's columns in the same order, so the merge's MFMA
+// pairs position p of u with position p of Wv.
+template <int CT>
+__device__ __forceinline__ void xstore_u(bf16* up, long long kstride, const f32x16 (&o)[CT], float inv, int hh) {
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) {
+      bf16x8 w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = f2bf(o[c][8 * gp + e] * inv);
+      *(bf16x8*)(up + (2 * c + gp) * kstride + 8 * hh) = w;
+    }
+}
 
 // One work item: rows of group `grp` x (row, head) m-tile `mt`, key tiles [tb, te) written as partial `split`.
 template <int QW, int NW, int DEPTH, bool F8, int ABL, bool CAP>
@@ -478,20 +503,8 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
       a.part_ml[2 * pi] = m_run;
       a.part_ml[2 * pi + 1] = l_run;
     }
-    // u column c = cb + 32 c' + 8 g + 4 hh + e lives in 16-column block c / 16 = cb/16 + 2 c' + (g >> 1) at
-    // position 8 (g & 1) + 4 hh + e; a block holds every row of the slab, so xcomb reads 32 rows x 32 B
-    // contiguously
-    const long long kstride = a.slab_rows * 16;
-    bf16* up = a.part_u + (((long long)split * a.H + hd) * (a.d / 16) + cb / 16) * kstride + (long long)row * 16 + 4 * hh;
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[c][4 * g + e] * inv);
-        *(bf16x4*)(up + (2 * c + (g >> 1)) * kstride + 8 * (g & 1)) = w;
-      }
+    xstore_u(a.part_u + (((long long)split * a.H + hd) * (a.d / 16) + cb / 16) * (a.slab_rows * 16) + (long long)row * 16,
+             a.slab_rows * 16, o, inv, hh);
   }
 }
 
@@ -519,117 +532,225 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------------
-// LDS-DMA form (bf16 cross memory, d = 1280: 8 waves x 160 columns; the default there).  The same work items, the
-// same per-wave MFMAs and the same fixed-order cross-wave sum as xattn_segment, so the same bits; what changes is
-// how E reaches LDS and where the S partials live:
+// LDS-DMA form (bf16 cross memory, d = 1280: 8 waves x 160 columns; the default there).  Per tile the same per-wave
+// MFMAs and the same fixed-order cross-wave sum as xattn_segment; what changes is how E reaches LDS, where the S
+// partials live, and how the work is cut:
 //   - each wave streams its 10 KB slice of a tile straight into LDS (10 global_load_lds_dwordx4 of 1 KiB; the
 //     image's chunk swizzle goes on the per-lane SOURCE address), two tiles ahead, into a ring of two 80 KB slots
 //     that fills the whole 160 KB LDS -- no staging registers, no ds_write of E;
 //   - after a wave has read its slice of the current tile (the S operand, and the U operand of rows 0-15), that part
 //     of the slice is dead, and the S partials (4 KB) and their sums (512 B) are written there;
 //   - a third barrier per tile (after every wave has read the sums) frees the slot, and each wave then issues its
-//     DMAs of tile + 2 into it: a tile's loads are in flight for about one and a half tiles of compute.
-// Waits are counted vmcnt + raw s_barrier (no barrier drains the DMA queue: MI355X_MICROARCH.md item 7); q' is
-// loaded by inline asm and waited for explicitly, because the compiler waits vmcnt(0) at the first use of an
-// ordinary load's result while LDS-DMA is in flight (cdna_hip_programming.md §5, "Pipelining across barriers").
+//     DMAs of tile + 2 into it: a tile's loads are in flight for about one and a half tiles of compute;
+//   - the work: a "lane" is a (window group, m-tile) pair, a "unit" one 32-position tile of a lane, units numbered
+//     lane-major (lane x n_tiles + tile).  A workgroup walks a contiguous range of units -- one segment per lane it
+//     touches, each segment one partial of its lane, merged by xcomb like a key split:
+//       items:  the ranges of xattn_kernel's work items (window group, key split, m-tile): one segment each;
+//       chunks (stream-K; greedy passes, one m-tile per window): the pass's units cut into P equal contiguous ranges,
+//               P = the CU count (one 160 KB workgroup per CU), so every CU streams for the whole launch.  Items left
+//               the last round part-empty (150 windows x 3 splits = 450 items on 256 CUs) and paid each item's
+//               start-up (~7 us, tools/xattn_bench); a chunk pays it once and crosses one or two window boundaries.
+//               Its pieces are a function of the whole pass (the window count), not of how the pass is sliced into
+//               launches; a window's pieces add in a different order than its key splits, so the two cuts agree to
+//               f32 rounding, not bit for bit.
+// Waits are counted vmcnt + raw s_barrier (no barrier drains the DMA queue: MI355X_MICROARCH.md item 7).  q' is an
+// ordinary load whose first use sits where a full wait costs nothing extra: hipcc waits vmcnt(0) at the first use of
+// an ordinary load's result while LDS-DMA is in flight (cdna_hip_programming.md §5, "Pipelining across barriers").
 #define XD_QW 160
 #define XD_NW 8
 #define XD_IMG (32 * XD_QW * 2)            // bytes of one wave's slice of a tile
 #define XD_LS (XD_IMG / 1024)              // its LDS-DMA instructions
 #define XD_SLOT (XD_NW * XD_IMG)
 
-template <bool NT, int ABL, bool CAP>
-__device__ __forceinline__ void xattn_segment_dma(const XAttnArgs& a, char* smem, int grp, int mt, int split, int tb,
-                                                  int te) {
+// stream-K cut of W units into P chunks: chunk c = units [xsk_begin(c), xsk_begin(c + 1)); xsk_chunk(g) holds unit g
+__host__ __device__ __forceinline__ long long xsk_begin(long long c, long long W, int P) { return c * W / P; }
+__host__ __device__ __forceinline__ int xsk_chunk(long long g, long long W, int P) { return (int)(((g + 1) * P - 1) / W); }
+
+template <int ABL = 0, bool CAP = false>
+__global__ __launch_bounds__(XD_NW * 64) void xattn_dma_kernel(XAttnArgs a) {
   constexpr int QW = XD_QW, NW = XD_NW, KS = QW / 16, CT = QW / 32, LDR = xldr(QW), CPR = QW / 8, IMG = XD_IMG,
                 LS = XD_LS, SLOT = XD_SLOT;
   static_assert(LDR == QW && IMG % 1024 == 0, "unpadded image rows, whole DMA instructions");
   static_assert(16 * 64 * 4 + 64 * 8 <= 16 * LDR * 2, "the S partials and sums fit in rows 0-15 of the slice");
+  static_assert(KS == 10 && LS == 10 && CT == 5, "the asm blocks and vmcnt immediates below are written for d = 1280");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * XD_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l32 = lane & 31;
-  const int M = a.G * a.H;
-  const int m = mt * 32 + l32;
-  const int row0 = grp * a.G;
-  int row = row0, hd = 0;
-  bool valid = m < M;
-  if (valid) {
-    const int ri = m / a.H;
-    row = row0 + ri;
-    hd = m - ri * a.H;
-    valid = !(a.done && a.done[a.row_hyp[row]]);
-  }
-  if (!__any(valid)) return;             // identical in all waves: uniform exit before any barrier
-  const int slot = a.hyp_slot[a.row_hyp[row0]];
-  const int cb = wv * QW;
   const int n_tiles = (a.T + 31) / 32;
-  const char* EB16 = (const char*)a.enc + ((long long)slot * n_tiles * NW + wv) * (long long)IMG;
-  {
-    const unsigned long long nq = __popcll(__ballot(valid && hh == 0));
-    if (a.stat && tid == 0) {
-      const long long npos = (long long)min(te * 32, a.T) - tb * 32;
-      unsigned long long by = nq * (unsigned long long)a.d * 2;
-      if (mt == 0) by += (unsigned long long)(npos * a.d * 2);
-      atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), by);
+  const int M = a.G * a.H;
+  const int cb = wv * QW;
+  // this workgroup's units [gb, ge), launch-relative
+  int gb, ge, chunk = 0, item_split = 0;
+  if (a.sk_W) {
+    int b = blockIdx.x;
+    if (a.sk_map) {                              // XCD-contiguous: XCD x walks chunks [x n / 8, (x + 1) n / 8)
+      const int n = gridDim.x, xcd = b & 7, q = n >> 3, r = n & 7;
+      b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
     }
-  }
-  bf16x8 qf[KS];
-  {
-    const bf16* qr = a.qp + ((long long)row * a.H + hd) * a.d + cb + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = *(const bf16x8*)(qr + 16 * s);     // unconditional: row, hd are clamped
+    chunk = a.sk_c0 + b;
+    const long long L0 = (long long)a.sk_lane0 * n_tiles;
+    gb = (int)(max(xsk_begin(chunk, a.sk_W, a.sk_P), L0) - L0);
+    ge = (int)(min(xsk_begin(chunk + 1, a.sk_W, a.sk_P), L0 + (long long)a.sk_lanes * n_tiles) - L0);
+    if (gb >= ge) return;
+  } else {
+    const int j = blockIdx.x >> 3;
+    const int item = (blockIdx.x & 7) * a.per_xcd + (a.rev ? a.per_xcd - 1 - j : j);
+    if (item >= a.n_items) return;
+    const int mt = item % a.n_mt, rest = item / a.n_mt;
+    item_split = rest % a.splits;
+    const int ln = (rest / a.splits) * a.n_mt + mt;
+    gb = ln * n_tiles + item_split * n_tiles / a.splits;
+    ge = ln * n_tiles + (item_split + 1) * n_tiles / a.splits;
   }
   // DMA i of a tile fills LDS bytes [1024 i, 1024 i + 1024) of the wave's slice: lane l writes image granule
-  // p = 64 i + l = (row r, slot s), which holds chunk c = s ^ ((r >> 2) & 3) of row r (xchunk is an involution)
-  int goff[LS];
-#pragma unroll
-  for (int i = 0; i < LS; ++i) {
-    const int p = 64 * i + lane, r = p / CPR, s = p - r * CPR;
-    goff[i] = (r * CPR + xchunk(r, s)) * 16;
-  }
-  auto issue = [&](int tile) {
-    const char* src = EB16 + (long long)tile * SLOT;
-    char* dst = smem + (tile & 1) * SLOT + wv * IMG;
-#pragma unroll
-    for (int i = 0; i < LS; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src + goff[i]), (__attribute__((address_space(3))) void*)(dst + 1024 * i),
-                                       16, 0, NT ? 2 : 0);
+  // p = 64 i + l = (row r, slot s), which holds chunk c = s ^ ((r >> 2) & 3) of row r (xchunk is an involution).
+  // CPR = 20 is a multiple of 4, so that source granule r CPR + c is p ^ ((r >> 2) & 3), r >> 2 = p / 80.  Computed
+  // at each issue from an opaque lane id (ten persistent offsets cost the registers the accumulators need).
+  static_assert(CPR == 20, "granule = p ^ ((p / 80) & 3) needs 20 chunks per row");
+  // the wave's slice of tile 0 of a lane's window (the slot is tile-blocked: xblock_kernel)
+  auto ebase = [&](int ln) -> const char* {
+    const int slot = a.hyp_slot[a.row_hyp[(ln / a.n_mt) * a.G]];
+    return (const char*)a.enc + ((long long)slot * n_tiles * NW + wv) * (long long)IMG;
   };
-  if constexpr ((ABL & 16) != 0) {       // compute-only ablation: finite constant images instead of loads
+  int lane_c = gb / n_tiles;                     // the current segment's lane
+  const char* base_c = ebase(lane_c);
+  const char* base_n = (lane_c + 1) * n_tiles < ge ? ebase(lane_c + 1) : base_c;
+  auto issue = [&](int g) {                      // unit g is in lane_c or lane_c + 1 (n_tiles >= 2)
+    const int lg = g / n_tiles;
+    const char* src = (lg == lane_c ? base_c : base_n) + (long long)(g - lg * n_tiles) * SLOT;
+    char* dst = smem + ((g - gb) & 1) * SLOT + wv * IMG;
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+#pragma unroll
+    for (int i = 0; i < LS; ++i) {
+      const int p = 64 * i + lo;
+      __builtin_amdgcn_global_load_lds((const void*)(src + 16 * (p ^ ((p / 80) & 3))),
+                                       (__attribute__((address_space(3))) void*)(dst + 1024 * i), 16, 0, 2 /* nt */);
+    }
+  };
+  // Segment state.  Chunks: every (row, head) column below M counts as valid whether its row is finished or not (its
+  // partial is stored and never merged: xcomb skips finished rows), so a segment's setup loads nothing but q'.
+  struct Seg {
+    int row, hd, piece;
+    bool valid;
+  };
+  auto seg_of = [&](int ln) -> Seg {
+    const int grp = ln / a.n_mt, mt = ln - grp * a.n_mt;
+    const int m = mt * 32 + l32, row0 = grp * a.G;
+    Seg sg{row0, 0, a.sk_W ? chunk - xsk_chunk((long long)(a.sk_lane0 + ln) * n_tiles, a.sk_W, a.sk_P) : item_split, m < M};
+    if (sg.valid) {
+      const int ri = m / a.H;
+      sg.row = row0 + ri;
+      sg.hd = m - ri * a.H;
+    }
+    return sg;
+  };
+  unsigned long long stat_bytes = 0;             // profiler bytes of this workgroup, one atomic at its end
+  auto count = [&](int ln, const Seg& sg, int g) {
+    const int tb = g - ln * n_tiles, te = min(n_tiles, ge - ln * n_tiles);
+    const unsigned long long nq = __popcll(__ballot(sg.valid && hh == 0));
+    const long long npos = (long long)min(te * 32, a.T) - tb * 32;
+    stat_bytes += nq * (unsigned long long)a.d * 2;
+    if (ln % a.n_mt == 0) stat_bytes += (unsigned long long)(npos * a.d * 2);
+  };
+  bf16x8 qf[KS];
+  auto load_q = [&](const Seg& sg) {             // unconditional: row, hd are clamped
+    const bf16* qr = a.qp + ((long long)sg.row * a.H + sg.hd) * a.d + cb + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = *(const bf16x8*)(qr + 16 * s);
+  };
+  // a use of q': the compiler waits vmcnt(0) here, and no later use of q' waits
+  auto q_landed = [&](const Seg& sg) {
+    asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]), "v"(qf[4]), "v"(qf[5]), "v"(qf[6]), "v"(qf[7]),
+                 "v"(qf[8]), "v"(qf[9]));
+    if (!sg.valid) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) qf[s] = bf16x8{};
+    }
+  };
+  float* pr_row = nullptr;
+  auto cap_row = [&](const Seg& sg) {            // alignment capture: the row's raw-score row (wave 0)
+    pr_row = nullptr;
+    if (CAP && a.probs && wv == 0 && sg.valid) {
+      const int hm = a.head_map[sg.hd];
+      if (hm >= 0) pr_row = a.probs + ((long long)sg.row * a.n_align + hm) * a.T;
+    }
+  };
+  f32x16 o[CT];
+  float m_run, l_run;
+  auto reset = [&] {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) o[c] = xzero16();
+    m_run = -INFINITY;
+    l_run = 0.f;
+  };
+  // the segment's partial: (m, l) and u / l as bf16.  Every wave holds the same m, l (the same S after the cross-wave
+  // sum), so every valid lane stores its column's pair (equal values); the wave issues 11 stores or none.
+  auto flush = [&](const Seg& sg) {
+    l_run += __shfl_xor(l_run, 32, 64);
+    if (sg.valid) {
+      const float inv = 1.0f / l_run;
+      const long long pi = ((long long)sg.piece * a.slab_rows + sg.row) * a.H + sg.hd;
+      *(float2*)(a.part_ml + 2 * pi) = float2{m_run, l_run};
+      xstore_u(a.part_u + (((long long)sg.piece * a.H + sg.hd) * (a.d / 16) + cb / 16) * (a.slab_rows * 16) +
+                   (long long)sg.row * 16,
+               a.slab_rows * 16, o, inv, hh);
+    }
+  };
+
+  Seg cur = seg_of(lane_c);
+  if (!a.sk_W) {                                 // items: finished rows skip, and a finished m-tile exits
+    if (cur.valid) cur.valid = !(a.done && a.done[a.row_hyp[cur.row]]);
+    if (!__any(cur.valid)) return;               // uniform in the workgroup
+  }
+  count(lane_c, cur, gb);
+  load_q(cur);
+  if constexpr ((ABL & 16) != 0) {               // compute-only ablation: finite constant images instead of loads
 #pragma unroll
     for (int i = 0; i < 2 * LS; ++i)
       *(i32x4*)(smem + (i / LS) * SLOT + wv * IMG + 1024 * (i % LS) + 16 * lane) = i32x4{0x3c003c00, 0x3c003c00, 0x3c003c00, 0x3c003c00};
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   } else {
-    issue(tb);
+    issue(gb);
   }
-  // A use of q' here: the compiler waits vmcnt(0) for it -- q' and the first tile, which the first tile needs anyway --
-  // and no later use waits.  Only then the second tile's DMAs (a whole tile of compute ahead of their use).
-  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]), "v"(qf[4]), "v"(qf[5]), "v"(qf[6]), "v"(qf[7]),
-               "v"(qf[8]), "v"(qf[9]));
-  static_assert(KS == 10 && LS == 10, "10 q' fragments; the vmcnt immediates count 10 DMAs per tile");
+  q_landed(cur);                                 // with the first tile, which the first tile needs anyway
+  cap_row(cur);
   if constexpr ((ABL & 16) == 0) {
-    if (tb + 1 < te) issue(tb + 1);
+    if (gb + 1 < ge) issue(gb + 1);              // a whole tile of compute ahead of its use
   }
-  if (!valid) {
-#pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = bf16x8{};
-  }
-  f32x16 o[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) o[c] = xzero16();
-  float m_run = -INFINITY, l_run = 0.f;
-  float* pr_row = nullptr;
-  if (a.probs && wv == 0 && valid) {
-    const int hm = a.head_map[hd];
-    if (hm >= 0) pr_row = a.probs + ((long long)row * a.n_align + hm) * a.T;
-  }
-  for (int tile = tb; tile < te; ++tile) {
+  reset();
+  // A mid-chunk boundary (chunks only) after unit g, the last of segment A:
+  //   tile g:     no DMA after barrier 3; after A's U MFMAs, B's q' loads and their wait (vmcnt(0): B's q' and the
+  //               DMA of g + 1, which tile g + 1 needs anyway), then the DMA of g + 2;
+  //   tile g + 1: after its barrier 3 and the DMA of g + 3, A's partial stores (A's o, m, l are still live: B's first
+  //               U MFMAs come after), then reset for B.
+  // Store acknowledgements are slow while the loads stream (tools/xattn_bench: ~12 us when waited for at once), so
+  // the stores are issued after two DMAs that the next two tile waits count past them: vmcnt(10 + 10) at g + 2 and
+  // g + 3 (every vector-memory operation retires in issue order: MI355X_MICROARCH.md, vmcnt), and only the wait at
+  // g + 4 covers them.
+  int flushed = -8, f_ops = 0;                   // unit whose barrier-3 point issued A's stores; their count (>= 10)
+  bool f_pending = false;
+  Seg fseg = cur;
+  // LDS reads and writes that the DMA's destination may alias are inline asm: the compiler gives the tr16 intrinsic
+  // no alias information and cannot tell the other accesses from the DMA's destination, and would wait vmcnt(0) --
+  // drain the DMA of the next tile -- before them.  Each asm block that loads waits for its own loads (lgkmcnt(0)) and
+  // marks its outputs early-clobber: an asm output that returns after the statement could be copied by the compiler
+  // before it arrives.
+  auto lds_addr = [](const void* p) -> unsigned {
+    return (unsigned)(size_t)(__attribute__((address_space(3))) const char*)p;
+  };
+  for (int g = gb;; ++g) {
     int lo = lane;
     asm volatile("" : "+v"(lo));
-    char* base = smem + (tile & 1) * SLOT;
+    const int tile = g - lane_c * n_tiles;
+    const bool more = g + 1 < ge, last = !more || tile == n_tiles - 1;    // last unit of this segment
+    char* base = smem + ((g - gb) & 1) * SLOT;
     bf16* sE = (bf16*)(base + wv * IMG);
     bf16* sER = sE + 16 * LDR;
-    if constexpr ((ABL & 16) == 0) {     // this wave's DMAs of the tile have landed (those of tile + 1 may not)
-      if (tile + 1 < te) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    if constexpr ((ABL & 16) == 0) {             // this wave's DMAs of the tile have landed: all but the younger ones
+      // (the DMA of g + 1, and a boundary's partial stores issued after this tile's DMA)
+      const int younger = (more ? 10 : 0) + (g == flushed + 1 || g == flushed + 2 ? f_ops : 0);
+      if (younger >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else if (younger >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     f32x16 sc = xzero16();
@@ -638,17 +759,8 @@ __device__ __forceinline__ void xattn_segment_dma(const XAttnArgs& a, char* smem
     const int lowc = 2 * (G4 & 1) + (gp >> 1);
     const int o0 = (4 * hh + gq) * LDR + 8 * (lowc ^ hh) + 4 * (gp & 1);
     const int o1 = (8 + 4 * hh + gq) * LDR + 8 * (lowc ^ (2 + hh)) + 4 * (gp & 1);
-    // LDS reads and writes that the DMA's destination may alias are inline asm: the compiler gives the tr16 intrinsic
-    // no alias information and cannot tell the other accesses from the DMA's destination, and would wait vmcnt(0) --
-    // drain the DMA of tile + 1 -- before them.  Each asm block that loads waits for its own loads (lgkmcnt(0)) and
-    // marks its outputs early-clobber: an asm output that returns after the statement could be copied by the compiler
-    // before it arrives.
-    auto lds_addr = [](const bf16* p) -> unsigned {
-      return (unsigned)(size_t)(__attribute__((address_space(3))) const bf16*)p;
-    };
     // the 5 column tiles' transposed fragments of one 16-row half image (two ds_read_b64_tr_b16 each, 64 B apart per c)
     auto ufrags = [&](const bf16* img, bf16x8 (&u)[CT]) {
-      static_assert(CT == 5, "the U fragment reads list 5 column tiles");
       xi32x2 v[10];
       asm volatile(
           "ds_read_b64_tr_b16 %0, %10\n\tds_read_b64_tr_b16 %1, %11\n\t"
@@ -664,67 +776,59 @@ __device__ __forceinline__ void xattn_segment_dma(const XAttnArgs& a, char* smem
 #pragma unroll
       for (int c = 0; c < CT; ++c) u[c] = __builtin_bit_cast(bf16x8, i32x4{v[2 * c][0], v[2 * c][1], v[2 * c + 1][0], v[2 * c + 1][1]});
     };
-    bf16x8 u0[CT];
+    // the 8 waves' float2 at byte offset `off` of their slices (slices 0-3 from pr, 4-7 from pr + 4 IMG), waited
+    static_assert(IMG * 3 + 4096 + 512 <= 65536, "4 slices within one 16-bit LDS offset");
+    auto read8 = [&](unsigned pr, auto offc, float2 (&t)[NW]) {
+      constexpr int off = decltype(offc)::value;
+      asm volatile(
+          "ds_read_b64 %0, %8 offset:%10\n\tds_read_b64 %1, %8 offset:%11\n\t"
+          "ds_read_b64 %2, %8 offset:%12\n\tds_read_b64 %3, %8 offset:%13\n\t"
+          "ds_read_b64 %4, %9 offset:%10\n\tds_read_b64 %5, %9 offset:%11\n\t"
+          "ds_read_b64 %6, %9 offset:%12\n\tds_read_b64 %7, %9 offset:%13\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7])
+          : "v"(pr), "v"(pr + 4 * IMG), "i"(off), "i"(off + IMG), "i"(off + 2 * IMG), "i"(off + 3 * IMG)
+          : "memory");
+    };
+    bf16x8 u0[CT], u1[CT];
     if constexpr ((ABL & 7) != 7) {
-      const int l32o = lo & 31, g = (l32o >> 2) & 3;
+      const int l32o = lo & 31, gg = (l32o >> 2) & 3;
       const bf16* rb = l32o < 16 ? sE + l32o * LDR : sER + (l32o - 16) * LDR;
-      const bf16* s0 = rb + 8 * (hh ^ g);
-      const bf16* s1 = rb + 8 * ((2 + hh) ^ g);
+      const bf16* s0 = rb + 8 * (hh ^ gg);
+      const bf16* s1 = rb + 8 * ((2 + hh) ^ gg);
       bf16x8 ea[KS];
 #pragma unroll
       for (int s = 0; s < KS; ++s) ea[s] = *(const bf16x8*)(((s & 1) ? s1 : s0) + 32 * (s >> 1));
-      ufrags(sE, u0);                                          // rows 0-15: their bytes are reused below
+      ufrags(sE, u0);                            // rows 0-15: their bytes are reused below
 #pragma unroll
       for (int s = 0; s < KS; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ea[s], qf[s], sc, 0, 0, 0);
-      // the partials into the dead rows 0-15 of this wave's slice (LDS is in order: after the reads above).  Stores as
-      // inline asm too: the compiler cannot tell them from the DMA's destination and would wait vmcnt(0) first.
+      // the partials into the dead rows 0-15 of this wave's slice (LDS is in order: after the reads above).  The
+      // compiler's hazard recognizer does not look into inline asm: the wait states between the last S MFMA writing
+      // sc and the first store reading it (a 16-pass MFMA's result read by a non-MFMA: 18) are spelled out.
       const unsigned px = lds_addr(sE) + 8 * lane;
-      // the compiler's hazard recognizer does not look into inline asm: the wait states between the last S MFMA
-      // writing sc and the first store reading it (a 16-pass MFMA's result read by a non-MFMA: 18) are spelled out
       asm volatile("s_nop 15\n\ts_nop 3" : "+v"(sc)::"memory");
 #define XD_W2(k_) asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(px), "v"(float2{sc[2 * k_], sc[2 * k_ + 1]}), "i"(512 * k_) : "memory")
       XD_W2(0); XD_W2(1); XD_W2(2); XD_W2(3); XD_W2(4); XD_W2(5); XD_W2(6); XD_W2(7);
 #undef XD_W2
       xbarrier<true>();
-      // wave w sums registers 2w, 2w + 1 over the waves in order 0..7 (xattn_segment's order); reads as asm as well
-      static_assert(NW == 8 && IMG * 3 + 4096 + 512 <= 65536, "4 slices within one 16-bit LDS offset");
-      // the 8 waves' float2 at byte offset `off` of their slices (slices 0-3 from pr, 4-7 from pr + 4 IMG), waited
-      auto read8 = [&](unsigned pr, auto offc, float2 (&t)[NW]) {
-        constexpr int off = decltype(offc)::value;
-        asm volatile(
-            "ds_read_b64 %0, %8 offset:%10\n\tds_read_b64 %1, %8 offset:%11\n\t"
-            "ds_read_b64 %2, %8 offset:%12\n\tds_read_b64 %3, %8 offset:%13\n\t"
-            "ds_read_b64 %4, %9 offset:%10\n\tds_read_b64 %5, %9 offset:%11\n\t"
-            "ds_read_b64 %6, %9 offset:%12\n\tds_read_b64 %7, %9 offset:%13\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7])
-            : "v"(pr), "v"(pr + 4 * IMG), "i"(off), "i"(off + IMG), "i"(off + 2 * IMG), "i"(off + 3 * IMG)
-            : "memory");
-      };
+      // wave w sums registers 2w, 2w + 1 over the waves in order 0..7 (xattn_segment's order)
       float2 t[NW];
-      {
-        read8(lds_addr((const bf16*)base) + 8 * (wv * 64 + lane), std::integral_constant<int, 0>{}, t);
-        float2 v = t[0];
+      read8(lds_addr(base) + 8 * (wv * 64 + lane), std::integral_constant<int, 0>{}, t);
+      float2 v = t[0];
 #pragma unroll
-        for (int w2 = 1; w2 < NW; ++w2) {
-          v.x += t[w2].x;
-          v.y += t[w2].y;
-        }
-        asm volatile("ds_write_b64 %0, %1 offset:4096" ::"v"(px), "v"(v) : "memory");
+      for (int w2 = 1; w2 < NW; ++w2) {
+        v.x += t[w2].x;
+        v.y += t[w2].y;
       }
+      asm volatile("ds_write_b64 %0, %1 offset:4096" ::"v"(px), "v"(v) : "memory");
       xbarrier<true>();
-      {
-        read8(lds_addr((const bf16*)base) + 8 * lane, std::integral_constant<int, 4096>{}, t);
+      read8(lds_addr(base) + 8 * lane, std::integral_constant<int, 4096>{}, t);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          sc[2 * k] = t[k].x;
-          sc[2 * k + 1] = t[k].y;
-        }
+      for (int k = 0; k < 8; ++k) {
+        sc[2 * k] = t[k].x;
+        sc[2 * k + 1] = t[k].y;
       }
-    }
-    bf16x8 u1[CT];
-    if constexpr ((ABL & 7) != 7) {
-      ufrags(sER, u1);                                         // rows 16-31: untouched by the partials
+      ufrags(sER, u1);                           // rows 16-31: untouched by the partials
     }
     const int t0 = tile * 32;
     if (t0 + 32 > a.T) {
@@ -739,11 +843,18 @@ __device__ __forceinline__ void xattn_segment_dma(const XAttnArgs& a, char* smem
         if (t < a.T) pr_row[t] = sc[r];
       }
     }
-    // every wave's reads of this slot are complete: its slices take tile + 2 (the CAP stores above are older than
-    // these DMAs, so the next tile's counted wait covers them)
+    // every wave's reads of this slot are complete: its slices take unit g + 2 (the CAP stores above are older than
+    // these DMAs, so the next tile's counted wait covers them).  At a segment's end that waits for the next q'.
     if constexpr ((ABL & 7) != 7) xbarrier<true>();
     if constexpr ((ABL & 16) == 0) {
-      if (tile + 2 < te) issue(tile + 2);
+      if (!(last && more) && g + 2 < ge) issue(g + 2);
+    }
+    if (f_pending) {                             // the previous segment's partial, after this tile's DMA (see above)
+      flush(fseg);
+      f_ops = __any(fseg.valid) ? 10 : 0;        // a lower bound of the store instructions issued (11 or 0)
+      flushed = g;
+      f_pending = false;
+      reset();
     }
     if constexpr ((ABL & 7) != 7) {
       float mx = sc[0];
@@ -773,47 +884,38 @@ __device__ __forceinline__ void xattn_segment_dma(const XAttnArgs& a, char* smem
         o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(u1[c], pf[1], o[c], 0, 0, 0);
       }
     }
-  }
-  l_run += __shfl_xor(l_run, 32, 64);
-  if (valid) {
-    const float inv = 1.0f / l_run;
-    const long long pi = ((long long)split * a.slab_rows + row) * a.H + hd;
-    if (wv == 0 && hh == 0) {
-      a.part_ml[2 * pi] = m_run;
-      a.part_ml[2 * pi + 1] = l_run;
-    }
-    const long long kstride = a.slab_rows * 16;
-    bf16* up = a.part_u + (((long long)split * a.H + hd) * (a.d / 16) + cb / 16) * kstride + (long long)row * 16 + 4 * hh;
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[c][4 * g + e] * inv);
-        *(bf16x4*)(up + (2 * c + (g >> 1)) * kstride + 8 * (g & 1)) = w;
+    if (last) {
+      if (!more) {
+        flush(cur);
+        break;
       }
+      // the next lane's segment (chunks only): A's partial waits for tile g + 1 (no partial is pending here: a
+      // pending one is stored at the first tile of its successor, before that tile's end); B's q' lands with the DMA
+      // of g + 1
+      fseg = cur;
+      f_pending = true;
+      cur = seg_of(lane_c + 1);
+      load_q(cur);                               // loaded and waited for in one block: a load whose wait the compiler
+                                                 // could not place before the loop's next use of q' would be waited
+                                                 // for (vmcnt(0)) at every tile
+      ++lane_c;
+      base_c = base_n;
+      base_n = (lane_c + 1) * n_tiles < ge ? ebase(lane_c + 1) : base_c;
+      count(lane_c, cur, g + 1);
+      q_landed(cur);
+      cap_row(cur);
+      if constexpr ((ABL & 16) == 0) {
+        if (g + 2 < ge) issue(g + 2);
+      }
+    }
   }
-}
-
-template <int ABL = 0, bool CAP = false>
-__global__ __launch_bounds__(XD_NW * 64) void xattn_dma_kernel(XAttnArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * XD_SLOT];
-  const int n_tiles = (a.T + 31) / 32;
-  const int j = blockIdx.x >> 3;
-  const int item = (blockIdx.x & 7) * a.per_xcd + (a.rev ? a.per_xcd - 1 - j : j);
-  if (item >= a.n_items) return;
-  const int mt = item % a.n_mt;
-  const int rest = item / a.n_mt;
-  const int split = rest % a.splits, grp = rest / a.splits;
-  const int tb = split * n_tiles / a.splits, te = (split + 1) * n_tiles / a.splits;
-  if (ABL == 0 && grp < a.keep) xattn_segment_dma<false, ABL, CAP>(a, smem, grp, mt, split, tb, te);
-  else xattn_segment_dma<true, ABL, CAP>(a, smem, grp, mt, split, tb, te);
+  if (a.stat && tid == 0) atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), stat_bytes);
 }
 
 // ------------------------------------------------------------------------------------------------------
 struct XCombArgs {
   const bf16* part_u; const float* part_ml; int splits; long long slab_rows;
+  long long sk_W; int sk_P, sk_lane0, n_tiles, G;   // LDS-DMA chunks: a row's piece count follows from its lane
   const bf16* wvb; const float* bv;      // this layer's V projection packed [H][d/16][64][16], bias [d]
   const int* row_hyp; const int* done;
   bf16* out; long long ldo;
@@ -842,7 +944,11 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
   const long long sstride = a.slab_rows * a.H;          // (row, head) pairs per split slab
   float w[MAXS];
   float Mx = -INFINITY, L = 0.f;
-  const int ns = a.splits;
+  int ns = a.splits;
+  if (a.sk_W) {                          // the chunks this row's window spans (xattn_dma_kernel)
+    const long long f = (long long)(a.sk_lane0 + rc / a.G) * a.n_tiles;
+    ns = xsk_chunk(f + a.n_tiles - 1, a.sk_W, a.sk_P) - xsk_chunk(f, a.sk_W, a.sk_P) + 1;
+  }
 #pragma unroll
   for (int s = 0; s < MAXS; ++s) w[s] = 0.f;
   {
@@ -1095,6 +1201,36 @@ int xattn_splits(int plan_rows, int group, int H, int T, int d) {
   return s;
 }
 
+// The factored attention's plan for a pass: the LDS-DMA chunk cut (stream-K, xattn_dma_kernel) where it applies --
+// `chunks_ok` (the engine: LDS-DMA form, bf16 cross memory, no cache-policy / walk-order experiment) and one m-tile
+// per window group -- else xattn_splits' key splits.  `slabs` = partial slabs the pass writes (scratch sizing, and
+// the merge's bound).  P = the CU count (one 160 KB workgroup per CU), at most one chunk per 7th of a window's tiles
+// so a window spans at most 8 chunks.
+XPlan xattn_plan(int plan_rows, int group, int H, int T, int d, bool chunks_ok) {
+  XPlan p;
+  p.slabs = xattn_splits(plan_rows, group, H, T, d);
+  if (!chunks_ok || d != XD_NW * XD_QW || group * H > 32 || plan_rows < group) return p;
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return std::max(1, n);
+  }();
+  const int n_tiles = (T + 31) / 32;
+  const long long W = (long long)(plan_rows / group) * n_tiles;
+  const int min_chunk = std::max(2, (n_tiles + 6) / 7);
+  static const int p_env = [] {                         // VLOG_AMD_XCHUNK_P: chunk count override (A/B)
+    const char* e = std::getenv("VLOG_AMD_XCHUNK_P");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int P = (int)std::max<long long>(1, std::min<long long>(p_env > 0 ? p_env : ncu, W / min_chunk));
+  const long long per = W / P;                           // >= min_chunk unless W < min_chunk (one chunk)
+  p.slabs = (int)std::min<long long>(XMAXS, (n_tiles + per - 1) / per + 1);
+  p.sk_W = W;
+  p.sk_P = P;
+  return p;
+}
+
 static int g_xattn_abl = [] {            // ablation / load-policy experiments (VLOG_AMD_XABL); product: 0
   const char* e = std::getenv("VLOG_AMD_XABL");
   return e ? std::atoi(e) : 0;
@@ -1102,13 +1238,17 @@ static int g_xattn_abl = [] {            // ablation / load-policy experiments (
 void xattn_set_ablation(int abl) { g_xattn_abl = abl; }
 
 void launch_xattn(const bf16* qp, const void* enc, const float* escale, const int* hyp_slot, const int* row_hyp,
-                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, int splits, int rev, int keep,
-                  int dma, bf16* part_u,
+                  const int* done, int rows, long long slab_rows, int group, int H, int T, int d, const XPlan& plan, int rev,
+                  int keep, int dma, int lane0, bf16* part_u,
                   float* part_ml, float* probs, const int* head_map, int n_align, unsigned long long* stat,
                   hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (rows <= 0) return;
   if (group <= 0 || rows % group != 0) throw std::runtime_error("xattn: rows must be a multiple of the group");
-  if (splits < 1 || splits > XMAXS || splits > (T + 31) / 32) throw std::runtime_error("xattn: bad key splits");
+  const int splits = plan.slabs, n_tiles = (T + 31) / 32;
+  if (splits < 1 || splits > XMAXS || (!plan.sk_W && splits > n_tiles)) throw std::runtime_error("xattn: bad key splits");
+  const bool dma_form = dma && !escale && d == XD_NW * XD_QW && keep == 0;
+  if (plan.sk_W && (!dma_form || group * H > 32 || lane0 < 0 || (long long)(lane0 + rows / group) * n_tiles > plan.sk_W))
+    throw std::runtime_error("xattn: chunk plan does not match the launch");
   XAttnArgs a{};
   a.qp = qp; a.enc = (const bf16*)enc; a.escale = escale; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
   a.H = H; a.T = T; a.d = d; a.G = group; a.n_mt = (group * H + 31) / 32; a.splits = splits; a.rev = rev; a.keep = keep;
@@ -1118,14 +1258,24 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
   a.per_xcd = (a.n_items + 7) / 8;
   a.slab_rows = slab_rows; a.part_u = part_u; a.part_ml = part_ml;
   a.probs = probs; a.head_map = head_map; a.n_align = n_align; a.stat = stat; a.abl = g_xattn_abl;
-  const dim3 grid(a.per_xcd * 8);
+  dim3 grid(a.per_xcd * 8);
+  if (plan.sk_W) {                       // the chunks that hold this launch's lanes (a sliced pass: the same pieces)
+    a.sk_W = plan.sk_W; a.sk_P = plan.sk_P; a.sk_lane0 = lane0; a.sk_lanes = rows / group;
+    const long long g0 = (long long)lane0 * n_tiles, g1 = (long long)(lane0 + a.sk_lanes) * n_tiles;
+    a.sk_c0 = xsk_chunk(g0, plan.sk_W, plan.sk_P);
+    static const int map_env = [] {       // XCD-contiguous chunks (default; 0: chunk = block id): 3-7 % faster in
+      const char* e = std::getenv("VLOG_AMD_XCHUNK_MAP");   // tools/xattn_bench at 128-256 windows
+      return e ? std::atoi(e) : 1;
+    }();
+    a.sk_map = map_env;
+    grid = dim3(xsk_chunk(g1 - 1, plan.sk_W, plan.sk_P) + 1 - a.sk_c0);
+  }
 #define XA_LAUNCH_C(QW_, NW_, DP_, F8_, CAP_)                                                                      \
   if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_, 0, CAP_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a); \
   else hipLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_, 0, CAP_>), grid, dim3(NW_ * 64), 0, st, a);
 #define XA_LAUNCH_F(QW_, NW_, DP_, F8_)                                                                            \
   if (probs) { XA_LAUNCH_C(QW_, NW_, DP_, F8_, true) } else { XA_LAUNCH_C(QW_, NW_, DP_, F8_, false) }
 #define XA_LAUNCH(QW_, NW_, DP_) XA_LAUNCH_F(QW_, NW_, DP_, false)
-  const bool dma_form = dma && !escale && d == XD_NW * XD_QW;
   if (a.abl) {                           // microbenchmark ablations (tools/xattn_bench): d = 1280, default form only
     if (d != 1280) throw std::runtime_error("xattn: ablations are built for n_state 1280 only");
     if (dma_form) {                      // LDS-DMA form: loads only (7) or compute only (16)
@@ -1190,12 +1340,14 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
   WM_LAUNCH_CHECK("xattn_kernel");
 }
 
-void launch_xcomb_vo(const bf16* part_u, const float* part_ml, int splits, long long slab_rows, const bf16* wvb,
-                     const float* bv, const int* row_hyp, const int* done, bf16* out, long long ldo, int rows, int group,
-                     int H, int d, int T, float* probs, const int* head_map, int n_align, hipStream_t st) {
+void launch_xcomb_vo(const bf16* part_u, const float* part_ml, const XPlan& plan, int lane0, long long slab_rows,
+                     const bf16* wvb, const float* bv, const int* row_hyp, const int* done, bf16* out, long long ldo, int rows,
+                     int group, int H, int d, int T, float* probs, const int* head_map, int n_align, hipStream_t st) {
   if (rows <= 0) return;
+  const int splits = plan.slabs;
   XCombArgs a{};
   a.part_u = part_u; a.part_ml = part_ml; a.splits = splits; a.slab_rows = slab_rows; a.wvb = wvb; a.bv = bv;
+  a.sk_W = plan.sk_W; a.sk_P = plan.sk_P; a.sk_lane0 = lane0; a.n_tiles = (T + 31) / 32; a.G = group;
   a.row_hyp = row_hyp; a.done = done; a.out = out; a.ldo = ldo; a.rows = rows; a.H = H; a.d = d; a.T = T;
   a.probs = probs; a.head_map = head_map; a.n_align = n_align;
   // 16-row blocks unless the grid already fills the chip with 32-row ones (VLOG_AMD_XCOMB_RT=32|16 forces)

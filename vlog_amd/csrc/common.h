@@ -66,6 +66,14 @@ struct CrossFuse {
                                    // the last-arriving split in-kernel (nullptr: separate combine kernel)
 };
 
+// The factored cross-attention's cut of a decoder pass (attn_xenc.hip xattn_plan): `slabs` partials per row (key splits,
+// or at most that many LDS-DMA chunk pieces); sk_W > 0: the stream-K chunk cut of sk_W units into sk_P chunks.
+struct XPlan {
+  int slabs = 1;
+  long long sk_W = 0;
+  int sk_P = 0;
+};
+
 // Launch check used by every host-side launcher: converts an asynchronous launch failure into an
 // exception the C-ABI layer turns into an error code + wm_last_error() text.
 #define WM_LAUNCH_CHECK(what)                                                                  \

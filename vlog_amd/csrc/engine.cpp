@@ -47,13 +47,14 @@ void launch_cross_attn(const bf16*, long long, const bf16*, const bf16*, int, co
 void launch_xpack(const bf16*, bf16*, bf16*, int, int, int, hipStream_t);
 void launch_xq(const bf16*, long long, const CrossFuse&, const bf16*, bf16*, int, int, int, hipStream_t);
 int xattn_splits(int, int, int, int, int);
+XPlan xattn_plan(int, int, int, int, int, bool);
 void launch_xquant8(const bf16*, long long, int, unsigned char*, float*, hipStream_t);
 long long xblock_slot_elems(int T, int d);
 void launch_xblock(const bf16* src, int B, int T, int d, bf16* dst, bool to_blocked, hipStream_t st);
-void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int, int, int, int,
-                  int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
-void launch_xcomb_vo(const bf16*, const float*, int, long long, const bf16*, const float*, const int*, const int*, bf16*,
-                     long long, int, int, int, int, int, float*, const int*, int, hipStream_t);
+void launch_xattn(const bf16*, const void*, const float*, const int*, const int*, const int*, int, long long, int, int, int, int,
+                  const XPlan&, int, int, int, int, bf16*, float*, float*, const int*, int, unsigned long long*, hipStream_t, hipEvent_t, hipEvent_t);
+void launch_xcomb_vo(const bf16*, const float*, const XPlan&, int, long long, const bf16*, const float*, const int*, const int*,
+                     bf16*, long long, int, int, int, int, int, float*, const int*, int, hipStream_t);
 
 void launch_token_probs(const float*, int, int, int, const int*, float*, hipStream_t);
 void launch_align_matrix(const float*, int, int, int, int, int, int, int, float*, float*, float*, hipStream_t);
@@ -248,8 +249,11 @@ struct wm_engine {
   int xkeep = 0;             // factored cross-attention: window groups whose encoder output is loaded with the default
                              // cache policy (the rest non-temporal), to keep them in the Infinity Cache across layers
   bool xsnake = false;       // factored cross-attention: odd layers walk each XCD's items in reverse (Infinity Cache reuse)
-  int xdma = 1;              // factored cross-attention, bf16 at n_state 1280: 1 = the LDS-DMA form (default), 0 = the
-                             // register-staged form (same bits; attn_xenc.hip)
+  int xdma = 0;              // factored cross-attention, bf16 at n_state 1280: 1 = the LDS-DMA form, 0 = the
+                             // register-staged form (default; same bits on key-split items; attn_xenc.hip).  Headline
+                             // A/B on one box (profiles/ab_r06_xattn_forms.jsonl): register 3773, LDS-DMA chunks 3752,
+                             // LDS-DMA key-split items 3711 RTFx
+  int xchunks = 1;           // ... LDS-DMA form, greedy passes: 1 = stream-K chunks, 0 = key-split items
   DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs (cross_fp8: OCP e4m3 bytes)
   DevBuf xscale;             // cross_fp8: [n_slots][T] f32 per-position scales
   int cross_fp8 = 0;         // opt-in fp8 cross memory (factored form only; changes numerics, never the default)
@@ -565,6 +569,12 @@ struct DecSlice {
 
 // Issues decoder layer l for one slice.  `mid` (optional) is recorded on the slice's stream right before its
 // cross-attention, which is where the second slice starts (see decoder_pass).
+// The factored cross-attention may cut a greedy pass into stream-K chunks (attn_xenc.hip xattn_plan): the LDS-DMA form
+// with bf16 cross memory and no cache-policy or walk-order experiment on
+static bool xattn_chunks_ok(const wm_engine* e) {
+  return e->xdma && e->xchunks && !e->cross_fp8 && e->xkeep == 0 && !e->xsnake;
+}
+
 void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, const int* row_hyp, const int* done,
                    const int* lin, const std::vector<std::vector<int>>* align_map, int n_align, float* attn,
                    int cross_group, hipEvent_t mid) {
@@ -785,7 +795,8 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
                       n_align, sl.total_rows, e->cross_cap, fz, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
   } else if (e->cross_mode == 1) {
     // factored: q' = Wk_h^T q_h, attention over the encoder output, split merge + Wv_h (attn_xenc.hip)
-    const int splits = xattn_splits(sl.total_rows, cross_group, H, T, d);
+    const XPlan plan = xattn_plan(sl.total_rows, cross_group, H, T, d, xattn_chunks_ok(e));
+    const int splits = plan.slabs;
     const size_t prow = (size_t)H * d;
     bf16* qp = e->s_qp.as<bf16>() + (size_t)r0 * prow;
     bf16* pu = e->s_pu.as<bf16>() + (size_t)r0 * 16;         // blocked layout: rows are 16-element records
@@ -800,11 +811,11 @@ void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, 
     {
       ProfScope ps(e, P_CROSS_ATTN, st, 0, 0, true);
       launch_xattn(qp, e->xenc.p, e->cross_fp8 ? e->xscale.as<float>() : nullptr, e->d_hyp_slot.as<int>(), row_hyp, done, rows, sl.total_rows, cross_group, H, T,
-                   d, splits, e->xsnake ? (l & 1) : 0, e->xkeep, e->xdma, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
+                   d, plan, e->xsnake ? (l & 1) : 0, e->xkeep, e->xdma, r0 / cross_group, pu, pml, probs, hmap, n_align, e->dstat(P_CROSS_ATTN), st, ps.a, ps.b);
     }
     {
       ProfScope ps(e, P_CROSS_COMB, st, 2.0 * rows * d * d, 2.0 * d * d + 2.0 * splits * rows * prow + 2.0 * rows * d);
-      launch_xcomb_vo(pu, pml, splits, sl.total_rows, wv, bv, row_hyp, done, ao, d, rows, cross_group, H, d, T, probs, hmap,
+      launch_xcomb_vo(pu, pml, plan, r0 / cross_group, sl.total_rows, wv, bv, row_hyp, done, ao, d, rows, cross_group, H, d, T, probs, hmap,
                       n_align, st);
     }
   } else {
@@ -865,7 +876,7 @@ void decoder_pass(wm_engine* e, int rows, const int* row_tok, const int* row_pos
     // per-head Wk^T layout (packed once per upload of dec.ckv.w)
     const int H = m.n_head, T = m.n_audio_ctx;
     const size_t prow = (size_t)H * d;
-    const int splits = xattn_splits(rows, cross_group, H, T, d);
+    const int splits = xattn_plan(rows, cross_group, H, T, d, xattn_chunks_ok(e)).slabs;
     e->s_qp.ensure((size_t)rows * prow * 2);
     e->s_pu.ensure((size_t)splits * rows * prow * 2);
     e->s_pml.ensure((size_t)splits * rows * H * 2 * 4);
@@ -2350,6 +2361,7 @@ int wm_create(const wm_model_dims* dims, int32_t device, wm_engine** out) {
     if (const char* v = std::getenv("VLOG_AMD_XSNAKE")) e->xsnake = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_XKEEP")) e->xkeep = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("VLOG_AMD_XDMA")) e->xdma = std::atoi(v) != 0;
+    if (const char* v = std::getenv("VLOG_AMD_XCHUNKS")) e->xchunks = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_CROSS_FP8")) e->cross_fp8 = std::atoi(v) != 0;
     if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_LDS")) e->dec_big_lds = std::atoi(v) == 144 ? 144 : 72;
     if (const char* v = std::getenv("VLOG_AMD_DEC_BIG_ROWS")) e->dec_big_rows = std::max(0, std::atoi(v));
@@ -2658,6 +2670,7 @@ int wm_set_option(wm_engine* e, const char* key, int64_t value) {
     else if (k == "cross_attn_snake") e->xsnake = value != 0;
     else if (k == "cross_attn_keep") e->xkeep = (int)std::max<int64_t>(0, std::min<int64_t>(value, 1 << 20));
     else if (k == "cross_attn_dma") e->xdma = value != 0;
+    else if (k == "cross_attn_chunks") e->xchunks = value != 0;
     else if (k == "gemm_persistent") gemm_8p_set_persistent((int)value);
     else if (k == "align_fused") align_set_fused((int)value);
     else if (k == "encode_chunk") e->enc_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
@@ -2738,6 +2751,7 @@ int wm_get_option(wm_engine* e, const char* key, int64_t* value) {
     else if (k == "cross_attn_snake") *value = e->xsnake;
     else if (k == "cross_attn_keep") *value = e->xkeep;
     else if (k == "cross_attn_dma") *value = e->xdma;
+    else if (k == "cross_attn_chunks") *value = e->xchunks;
     else if (k == "gemm_persistent") *value = gemm_8p_get_persistent();
     else if (k == "align_fused") *value = align_get_fused();
     else if (k == "encode_chunk") *value = e->enc_chunk;
