@@ -569,7 +569,7 @@ def main():
                          "model; same kernels and token counts, but near-tied logits (the parity gates cannot hold)")
     ap.add_argument("--check-every", type=int, default=4, help="decode steps between host polls of the live count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: profiles/traffic_r06.json, "
+    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: profiles/traffic_r06_b.json, "
                     "or traffic_r02_fp8.json with --cross-fp8)")
     ap.add_argument("--cross-fp8", action="store_true", help="opt-in fp8 (e4m3) cross memory: not the headline")
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-kernel event timing")
@@ -600,7 +600,7 @@ def main():
     if args.traffic_json is None:
         # the committed PMC files were measured on the default workload (uniform greedy, 150 windows); another
         # workload's launches move other bytes, so its line carries traffic null unless a file is given
-        args.traffic_json = (os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r06.json")
+        args.traffic_json = (os.path.join(ROOT, "profiles", "traffic_r02_fp8.json" if args.cross_fp8 else "traffic_r06_b.json")
                              if args.beam == 1 and args.workload == "uniform" and args.windows == 150 else "")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
