@@ -279,9 +279,11 @@ int wm_profile(wm_engine* e, int32_t enable);
  *   "cross_attn_dma" (default 0): 1 = at n_state 1280 with bf16 cross memory, the factored cross-attention streams the
  *   encoder output straight into LDS (LDS-DMA, two tiles ahead); 0 runs the register-staged form.  Bit-identical on
  *   key-split items; measured slower in the bench step.
- *   "cross_attn_chunks" (default 1): with the LDS-DMA form, greedy passes cut their (window, 32-position tile) units into
- *   one contiguous chunk per CU (stream-K) instead of per-window key splits; the pieces of a window are merged like
- *   key splits, so results agree to f32 rounding, not bit for bit.  0 = key splits.
+ *   "cross_attn_chunks" (default 0): 1 = at n_state 1280, greedy passes cut their (window, 32-position tile) units into
+ *   one contiguous chunk per CU (stream-K) instead of per-window key splits (the register form runs a chunk's
+ *   segments as work items, the LDS-DMA form walks a chunk per workgroup; the two give the same bits); the pieces
+ *   of a window are merged like key splits, so results agree with the key-split cut to f32 rounding, not bit for
+ *   bit.  Measured slower at the headline's 150 windows.
  *   "cross_attn_blocks" (default 0): grid cap of the cross-attention kernel, which walks its
  *   (window, head, key split) items with a grid stride; 0 launches one block per item.
  *   "cross_attn_fuse" (default 1): bit 0 folds the cq projection's split-K combine into the cross-attention

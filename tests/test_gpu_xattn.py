@@ -221,10 +221,11 @@ def test_large_v3_dma_form_bit_identical():
     (the default), both on key-split items (cross_attn_chunks 0): the same work items, per-wave MFMAs and
     fixed-order cross-wave sums, so the same bits -- teacher-forced logits over a 40-row prompt (two m-tiles per
     window), alignment-head capture on the attention kernel (cross_tf 0), greedy and beam-5 decodes (1 and 5 rows per
-    window, rows finishing at different steps).  Then its stream-K chunk cut for greedy passes: beam and
-    teacher-forced passes are untouched (more than one m-tile per window: items), greedy agrees to f32 rounding (a
-    window's pieces differ from its key splits), and slicing a pass into two launches (decode_split: 32 greedy rows,
-    two slices of 16) changes no bit."""
+    window, rows finishing at different steps).  Then the stream-K chunk cut for greedy passes (opt-in): the
+    register form (a chunk's segments as work items) and the LDS-DMA form (a workgroup walks its chunk) give the
+    same bits; beam and teacher-forced passes are untouched (more than one m-tile per window: items); greedy agrees
+    with the key-split cut to f32 rounding (a window's pieces differ from its key splits); and slicing a pass into
+    two launches (decode_split: 32 greedy rows, two slices of 16) changes no bit."""
     W, WB = 32, 4                                     # greedy over 32 windows, beam over 4
     dims, sd, eng, enc = _engine("large-v3", 2, W, eot_after=30)
     del sd
@@ -233,10 +234,10 @@ def test_large_v3_dma_form_bit_identical():
     toks = np.array([[st.sot, st.lang_token("en"), st.transcribe, st.no_timestamps] + list(range(500 + 40 * i, 536 + 40 * i))
                      for i in range(2)])
     prompt = [st.sot, st.lang_token("en"), st.transcribe]
-    assert eng.option("cross_attn_dma") == 0 and eng.option("cross_attn_chunks") == 1
+    assert eng.option("cross_attn_dma") == 0 and eng.option("cross_attn_chunks") == 0     # the defaults
     out = {}
     try:
-        for form, chunks, split in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)):
+        for form, chunks, split in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (0, 1, 1)):
             eng.set_option("cross_attn_dma", form)
             eng.set_option("cross_attn_chunks", chunks)
             eng.set_option("decode_split", split)
@@ -252,7 +253,7 @@ def test_large_v3_dma_form_bit_identical():
             out[(form, chunks, split)] = (lg.cpu().numpy(), at.cpu().numpy(), g, b, one)
     finally:
         eng.set_option("cross_attn_dma", 0)
-        eng.set_option("cross_attn_chunks", 1)
+        eng.set_option("cross_attn_chunks", 0)
         eng.set_option("decode_split", 0)
         eng.set_option("cross_tf", 1)
 
@@ -266,9 +267,11 @@ def test_large_v3_dma_form_bit_identical():
             assert [r.score for r in ra] == [r.score for r in rb]
             assert [r.no_speech_prob for r in ra] == [r.no_speech_prob for r in rb]
 
-    reg, items, chunks, sliced = out[(0, 0, 0)], out[(1, 0, 0)], out[(1, 1, 0)], out[(1, 1, 1)]
+    reg, items, chunks, dchunks, sliced = (out[(0, 0, 0)], out[(1, 0, 0)], out[(0, 1, 0)], out[(1, 1, 0)],
+                                           out[(0, 1, 1)])
     assert np.all(np.isfinite(items[0])) and np.allclose(items[1].sum(-1), 1.0, atol=1e-4)
-    same(reg, items)
+    same(reg, items)                  # the two forms on key-split items
+    same(chunks, dchunks)             # ... and on the chunk cut (register: segments as items; LDS-DMA: chunk walks)
     same(items, chunks, greedy=False)
     same(chunks, sliced)
     # the chunk cut vs the key splits on the same one-row-per-window pass: f32 rounding of the piece merge, then bf16

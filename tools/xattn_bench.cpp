@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
     for (int abl : abls) {
       xattn_set_ablation(abl);
       for (int splits : split_list) {
-        XPlan plan = xattn_plan(W, 1, H, T, d, !f8 && dma && sk && !snake && !keep);
+        XPlan plan = xattn_plan(W, 1, H, T, d, !f8 && sk && !snake && !keep);
         if (!plan.sk_W) plan.slabs = splits;
         auto run = [&] {
           launch_xattn(qp, enc, f8 ? scale : nullptr, slot, rh, nullptr, W, W, 1, H, T, d, plan, snake ? (launch_no++ & 1) : 0, keep, dma, 0, pu, pml,
@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = 1000.0 * ms / iters;
         printf("%s%s%s abl %2d splits %2d  %8.2f us  %7.1f GB/s (encoder output)\n", f8 ? "fp8 " : "bf16",
-               plan.sk_W ? " dma chunks" : !f8 && dma ? " dma" : "", snake ? " snake" : "", abl, plan.sk_W ? plan.sk_P : splits, us,
+               plan.sk_W ? (dma ? " dma chunks" : " chunk items") : !f8 && dma ? " dma" : "", snake ? " snake" : "", abl, plan.sk_W ? plan.sk_P : splits, us,
                bytes / (us * 1e-6) / 1e9);
       }
     }

@@ -218,7 +218,7 @@ struct XAttnArgs {
   float* part_ml;                        // [splits][slab_rows][H][2]   (m_s, l_s)
   float* probs; const int* head_map; int n_align;   // capture: raw scores [row][n_align][T]
   unsigned long long* stat;
-  long long sk_W; int sk_P, sk_lane0, sk_lanes, sk_c0, sk_map;   // LDS-DMA chunks (stream-K): units of the whole pass, chunk count,
+  long long sk_W; int sk_P, sk_lane0, sk_lanes, sk_c0, sk_nch, sk_map;   // LDS-DMA chunks (stream-K): units of the whole pass, chunk count,
                                          // this launch's first lane (of the pass) and lane count, its first chunk; sk_W = 0: items
   int abl;                               // microbenchmark ablations (tools/xattn_bench; product: 0, and the
                                          // product kernel is compiled without them: template ABL): bit 0 skips
@@ -508,6 +508,63 @@ __device__ __forceinline__ void xattn_segment(const XAttnArgs& a, char* smem, in
   }
 }
 
+// stream-K cut of W units into P chunks: chunk c = units [xsk_begin(c), xsk_begin(c + 1)); xsk_chunk(g) holds unit g
+__host__ __device__ __forceinline__ long long xsk_begin(long long c, long long W, int P) { return c * W / P; }
+__host__ __device__ __forceinline__ int xsk_chunk(long long g, long long W, int P) { return (int)(((g + 1) * P - 1) / W); }
+
+// The chunk cut's segments as separate work items (the register form; xattn_dma_kernel walks a chunk in one
+// workgroup instead).  XCD x (block id & 7) takes the contiguous chunk range [c_x, c_x + n_x) of the launch: its items
+// j < n_x are those chunks' first segments (from the chunk's start to the end of its lane or of the chunk), then one
+// item per lane start strictly inside the range (that lane's first piece, to the end of the chunk or of the lane;
+// an item whose lane start opens a chunk is empty).  The hardware hands an XCD's items to its CUs in block order, so
+// the CUs that finish a short first segment first take the second segments: per CU about one chunk of units and at
+// most two item start-ups, instead of ceil(items / CUs) rounds of equal items.  Segments, pieces and their order
+// per lane are those of xattn_dma_kernel's chunks, so the two forms give the same bits.  -> false: empty item.
+__device__ __forceinline__ bool xsk_item(const XAttnArgs& a, int n_tiles, int& lane, int& tb, int& te, int& piece) {
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int q = a.sk_nch >> 3, r = a.sk_nch & 7;
+  const int cx0 = a.sk_c0 + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q), ncx = q + (x < r ? 1 : 0);
+  const long long L0 = (long long)a.sk_lane0 * n_tiles, L1 = L0 + (long long)a.sk_lanes * n_tiles;
+  long long g0, g1;
+  if (j < ncx) {
+    const int c = cx0 + j;
+    g0 = max(xsk_begin(c, a.sk_W, a.sk_P), L0);
+    g1 = min(xsk_begin(c + 1, a.sk_W, a.sk_P), L1);
+    if (g0 >= g1) return false;
+    const long long la = g0 / n_tiles;
+    g1 = min(g1, (la + 1) * n_tiles);
+  } else {
+    const long long lo = max(xsk_begin(cx0, a.sk_W, a.sk_P), L0 + 1), hi = min(xsk_begin(cx0 + ncx, a.sk_W, a.sk_P), L1);
+    const long long la = (lo + n_tiles - 1) / n_tiles + (j - ncx);
+    g0 = la * n_tiles;
+    if (g0 >= hi) return false;
+    const int c = xsk_chunk(g0, a.sk_W, a.sk_P);
+    if (xsk_begin(c, a.sk_W, a.sk_P) == g0) return false;          // the chunk's own first segment covers it
+    g1 = min(min(xsk_begin(c + 1, a.sk_W, a.sk_P), L1), g0 + n_tiles);
+  }
+  const long long la = g0 / n_tiles;
+  lane = (int)(la - a.sk_lane0);
+  tb = (int)(g0 - la * n_tiles);
+  te = (int)(g1 - la * n_tiles);
+  piece = xsk_chunk(g0, a.sk_W, a.sk_P) - xsk_chunk(la * n_tiles, a.sk_W, a.sk_P);
+  return true;
+}
+
+// Blocks of a chunk-cut launch of the register form: 8 x the largest XCD item list (chunks + lane starts inside them).
+int xsk_item_blocks(long long W, int P, int c0, int nch, int lane0, int lanes, int n_tiles) {
+  const int q = nch >> 3, r = nch & 7;
+  const long long L0 = (long long)lane0 * n_tiles, L1 = L0 + (long long)lanes * n_tiles;
+  long long most = 0;
+  for (int x = 0; x < 8; ++x) {
+    const int cx0 = c0 + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q), ncx = q + (x < r ? 1 : 0);
+    if (ncx == 0) continue;
+    const long long lo = std::max(xsk_begin(cx0, W, P), L0 + 1), hi = std::min(xsk_begin(cx0 + ncx, W, P), L1);
+    const long long starts = hi > lo ? (hi + n_tiles - 1) / n_tiles - (lo + n_tiles - 1) / n_tiles : 0;
+    most = std::max(most, (long long)ncx + std::max(0LL, starts));
+  }
+  return (int)(8 * most);
+}
+
 template <int QW, int NW, int DEPTH, bool F8 = false, int ABL = 0, bool CAP = false>
 __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   static_assert(DEPTH == 1, "one tile staged ahead (the other staging forms are retired: DESIGN.md §6)");
@@ -515,6 +572,12 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
   constexpr int IMGR = 32;
   __shared__ __attribute__((aligned(16))) char smem[NW * IMGR * LDR * 2 + (NW + 1) * 16 * 64 * 4 + (F8 ? NW * 32 * 4 : 0)];
   const int n_tiles = (a.T + 31) / 32;
+  if (a.sk_W) {                                  // the chunk cut (greedy passes: one m-tile per window group)
+    int ln, tb, te, piece;
+    if (!xsk_item(a, n_tiles, ln, tb, te, piece)) return;
+    xattn_segment<QW, NW, DEPTH, F8, ABL, CAP>(a, smem, ln / a.n_mt, ln % a.n_mt, piece, tb, te);
+    return;
+  }
   // XCD-aware item order: the blocks of one (group, split), i.e. its m-tiles, run on one XCD at about the
   // same time, so the 2nd..n-th reads of an E tile hit that XCD's L2
   const int j = blockIdx.x >> 3;
@@ -562,9 +625,6 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 #define XD_LS (XD_IMG / 1024)              // its LDS-DMA instructions
 #define XD_SLOT (XD_NW * XD_IMG)
 
-// stream-K cut of W units into P chunks: chunk c = units [xsk_begin(c), xsk_begin(c + 1)); xsk_chunk(g) holds unit g
-__host__ __device__ __forceinline__ long long xsk_begin(long long c, long long W, int P) { return c * W / P; }
-__host__ __device__ __forceinline__ int xsk_chunk(long long g, long long W, int P) { return (int)(((g + 1) * P - 1) / W); }
 
 template <int ABL = 0, bool CAP = false>
 __global__ __launch_bounds__(XD_NW * 64) void xattn_dma_kernel(XAttnArgs a) {
@@ -1247,7 +1307,8 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
   const int splits = plan.slabs, n_tiles = (T + 31) / 32;
   if (splits < 1 || splits > XMAXS || (!plan.sk_W && splits > n_tiles)) throw std::runtime_error("xattn: bad key splits");
   const bool dma_form = dma && !escale && d == XD_NW * XD_QW && keep == 0;
-  if (plan.sk_W && (!dma_form || group * H > 32 || lane0 < 0 || (long long)(lane0 + rows / group) * n_tiles > plan.sk_W))
+  if (plan.sk_W && (keep != 0 || rev != 0 || group * H > 32 || lane0 < 0 ||
+                    (long long)(lane0 + rows / group) * n_tiles > plan.sk_W))
     throw std::runtime_error("xattn: chunk plan does not match the launch");
   XAttnArgs a{};
   a.qp = qp; a.enc = (const bf16*)enc; a.escale = escale; a.hyp_slot = hyp_slot; a.row_hyp = row_hyp; a.done = done;
@@ -1263,12 +1324,15 @@ void launch_xattn(const bf16* qp, const void* enc, const float* escale, const in
     a.sk_W = plan.sk_W; a.sk_P = plan.sk_P; a.sk_lane0 = lane0; a.sk_lanes = rows / group;
     const long long g0 = (long long)lane0 * n_tiles, g1 = (long long)(lane0 + a.sk_lanes) * n_tiles;
     a.sk_c0 = xsk_chunk(g0, plan.sk_W, plan.sk_P);
+    a.sk_nch = xsk_chunk(g1 - 1, plan.sk_W, plan.sk_P) + 1 - a.sk_c0;
     static const int map_env = [] {       // XCD-contiguous chunks (default; 0: chunk = block id): 3-7 % faster in
       const char* e = std::getenv("VLOG_AMD_XCHUNK_MAP");   // tools/xattn_bench at 128-256 windows
       return e ? std::atoi(e) : 1;
     }();
     a.sk_map = map_env;
-    grid = dim3(xsk_chunk(g1 - 1, plan.sk_W, plan.sk_P) + 1 - a.sk_c0);
+    // the LDS-DMA kernel walks a chunk per workgroup; the register form takes its segments as items (xsk_item)
+    grid = dma_form ? dim3(a.sk_nch)
+                    : dim3(xsk_item_blocks(plan.sk_W, plan.sk_P, a.sk_c0, a.sk_nch, lane0, a.sk_lanes, n_tiles));
   }
 #define XA_LAUNCH_C(QW_, NW_, DP_, F8_, CAP_)                                                                      \
   if (ev0) hipExtLaunchKernelGGL((xattn_kernel<QW_, NW_, DP_, F8_, 0, CAP_>), grid, dim3(NW_ * 64), 0, st, ev0, ev1, 0, a); \

@@ -253,7 +253,9 @@ struct wm_engine {
                              // register-staged form (default; same bits on key-split items; attn_xenc.hip).  Headline
                              // A/B on one box (profiles/ab_r06_xattn_forms.jsonl): register 3773, LDS-DMA chunks 3752,
                              // LDS-DMA key-split items 3711 RTFx
-  int xchunks = 1;           // ... LDS-DMA form, greedy passes: 1 = stream-K chunks, 0 = key-split items
+  int xchunks = 0;           // ... greedy passes at n_state 1280: 1 = the stream-K chunk cut (register form: its
+                             // segments as items; LDS-DMA form: a chunk per workgroup), 0 = key-split items (default:
+                             // the chunk cut loses at 150 windows, profiles/xattn_bench_r06_chunk_items.txt)
   DevBuf xenc;               // factored: [n_slots][T][d] bf16 encoder outputs (cross_fp8: OCP e4m3 bytes)
   DevBuf xscale;             // cross_fp8: [n_slots][T] f32 per-position scales
   int cross_fp8 = 0;         // opt-in fp8 cross memory (factored form only; changes numerics, never the default)
@@ -569,10 +571,10 @@ struct DecSlice {
 
 // Issues decoder layer l for one slice.  `mid` (optional) is recorded on the slice's stream right before its
 // cross-attention, which is where the second slice starts (see decoder_pass).
-// The factored cross-attention may cut a greedy pass into stream-K chunks (attn_xenc.hip xattn_plan): the LDS-DMA form
-// with bf16 cross memory and no cache-policy or walk-order experiment on
+// The factored cross-attention may cut a greedy pass into stream-K chunks (attn_xenc.hip xattn_plan): bf16 cross
+// memory, no cache-policy or walk-order experiment on
 static bool xattn_chunks_ok(const wm_engine* e) {
-  return e->xdma && e->xchunks && !e->cross_fp8 && e->xkeep == 0 && !e->xsnake;
+  return e->xchunks && !e->cross_fp8 && e->xkeep == 0 && !e->xsnake;
 }
 
 void decoder_layer(wm_engine* e, const DecSlice& sl, int l, const int* row_pos, const int* row_hyp, const int* done,
