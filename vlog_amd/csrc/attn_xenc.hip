@@ -1230,11 +1230,22 @@ void launch_xq(const bf16* q, long long ldq, const CrossFuse& fz, const bf16* wk
   WM_LAUNCH_CHECK("xq_kernel");
 }
 
+// CUs of the current device (one item per CU at a time: the kernels' LDS allows one workgroup per CU)
+static int xattn_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return std::max(1, v);
+  }();
+  return n;
+}
+
 // Key splits of a pass.  A function of the whole pass, so slicing a pass into launches never changes a
-// row's arithmetic: about 1.75 rounds of 256 one-workgroup CUs (at most 8) (measured on the 150-window large-v3
-// decode: 1 / 2 / 3 / 4 / 5 splits -> 522 / 564 / 450 / 510 / 483 ms of attention per bench step; fewer,
-// longer items amortise each item's prologue and epilogue, more of them fill the last round), at most 16,
-// at least one 32-position tile per split, and the bf16 partial slabs capped at 256 MB.
+// row's arithmetic: the count that minimises the launch model below (round 5: about 1.75 rounds of 256
+// one-workgroup CUs; measured on the 150-window large-v3 decode: 1 / 2 / 3 / 4 / 5 splits -> 522 / 564 / 450 /
+// 510 / 483 ms of attention per bench step), at most 8, at least one 32-position tile per split, and the bf16
+// partial slabs capped at 256 MB.
 int xattn_splits(int plan_rows, int group, int H, int T, int d) {
   static const int forced = [] {
     const char* e = std::getenv("VLOG_AMD_XSPLITS");
@@ -1253,9 +1264,38 @@ int xattn_splits(int plan_rows, int group, int H, int T, int d) {
   const long long n_mt = ((long long)group * H + 31) / 32;
   const long long items = groups * n_mt;
   const int n_tiles = (T + 31) / 32;
+  // Round 6: the split count minimises a measured model of the launch (tools/xattn_bench key-split sweep over 16-200
+  // windows, profiles/xattn_bench_r06_split_sweep.txt): the items run in rounds of one per CU, an item of n tiles
+  // takes 5.7 + n t us (t = 3.2 with the chip full, 2.87 with fewer than 94 % of the CUs busy), and the merge reads
+  // one partial per row and split (0.017 us each).  It fills ONE round where it can (64 windows: 4 splits, 45.0 us
+  // against 57.9 for the round-5 rule's 7; 128: 2, 80.5 against 96.9) and keeps 3 at the headline's 150.
+  // VLOG_AMD_XSPLITS_RULE=0: the round-5 rule (about 1.75 rounds, A/B).
+  static const int rule_env = [] {
+    const char* e = std::getenv("VLOG_AMD_XSPLITS_RULE");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int s_max = std::max(1, std::min(std::min(cap, XMAXS), n_tiles));
   int s = (int)((448 + items / 2) / items);
+  if (rule_env && n_mt == 1) {                  // greedy decode passes (the model was measured on one m-tile per window;
+                                                // a prompt pass's m-tiles share E in L2: 3 splits instead of 1 at 150
+                                                // windows x 3 rows cost the uniform bench 0.7 %, ab_r06_xsplits_rule)
+    const long long cus = xattn_cus();
+    double best = 1e300;
+    for (int c = 1; c <= s_max; ++c) {
+      const double tiles = (double)n_tiles / c;
+      double t = 0.017 * plan_rows * c;
+      for (long long left = items * c; left > 0; left -= cus) {
+        const long long busy = std::min(left, cus);
+        t += 5.7 + tiles * (busy * 100 >= cus * 94 ? 3.2 : 2.87);
+      }
+      if (t < best - 1e-9) {
+        best = t;
+        s = c;
+      }
+    }
+  }
   if (forced > 0) s = forced;
-  s = std::max(1, std::min(s, std::min(std::min(cap, XMAXS), n_tiles)));
+  s = std::max(1, std::min(s, s_max));
   const long long slab = (long long)plan_rows * H * d * 2;
   while (s > 1 && slab * s > (256LL << 20)) --s;
   return s;
@@ -1270,12 +1310,7 @@ XPlan xattn_plan(int plan_rows, int group, int H, int T, int d, bool chunks_ok) 
   XPlan p;
   p.slabs = xattn_splits(plan_rows, group, H, T, d);
   if (!chunks_ok || d != XD_NW * XD_QW || group * H > 32 || plan_rows < group) return p;
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 256;
-    return std::max(1, n);
-  }();
+  const int ncu = xattn_cus();
   const int n_tiles = (T + 31) / 32;
   const long long W = (long long)(plan_rows / group) * n_tiles;
   const int min_chunk = std::max(2, (n_tiles + 6) / 7);
