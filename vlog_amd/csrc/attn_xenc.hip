@@ -595,7 +595,8 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------------
-// LDS-DMA form (bf16 cross memory, d = 1280: 8 waves x 160 columns; the default there).  Per tile the same per-wave
+// LDS-DMA form (opt-in, cross_attn_dma; bf16 cross memory, d = 1280: 8 waves x 160 columns; measured slower than the
+// register form in the bench step).  Per tile the same per-wave
 // MFMAs and the same fixed-order cross-wave sum as xattn_segment; what changes is how E reaches LDS, where the S
 // partials live, and how the work is cut:
 //   - each wave streams its 10 KB slice of a tile straight into LDS (10 global_load_lds_dwordx4 of 1 KiB; the
@@ -615,7 +616,8 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 //               start-up (~7 us, tools/xattn_bench); a chunk pays it once and crosses one or two window boundaries.
 //               Its pieces are a function of the whole pass (the window count), not of how the pass is sliced into
 //               launches; a window's pieces add in a different order than its key splits, so the two cuts agree to
-//               f32 rounding, not bit for bit.
+//               f32 rounding, not bit for bit.  A mid-chunk window boundary costs ~10 us (the finished segment's
+//               partial stores are acknowledged late while every CU streams, and later DMA waits count them).
 // Waits are counted vmcnt + raw s_barrier (no barrier drains the DMA queue: MI355X_MICROARCH.md item 7).  q' is an
 // ordinary load whose first use sits where a full wait costs nothing extra: hipcc waits vmcnt(0) at the first use of
 // an ordinary load's result while LDS-DMA is in flight (cdna_hip_programming.md §5, "Pipelining across barriers").
@@ -624,7 +626,6 @@ __global__ __launch_bounds__(NW * 64) void xattn_kernel(XAttnArgs a) {
 #define XD_IMG (32 * XD_QW * 2)            // bytes of one wave's slice of a tile
 #define XD_LS (XD_IMG / 1024)              // its LDS-DMA instructions
 #define XD_SLOT (XD_NW * XD_IMG)
-
 
 template <int ABL = 0, bool CAP = false>
 __global__ __launch_bounds__(XD_NW * 64) void xattn_dma_kernel(XAttnArgs a) {
