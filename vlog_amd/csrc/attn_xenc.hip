@@ -992,7 +992,11 @@ struct XCombArgs {
 // RT = rows per block, 32 or 16.  With 16, MFMA rows 16..31 repeat rows 0..15 (same addresses: no extra bytes)
 // and are not stored, so every output keeps the 32-row form's arithmetic bit for bit while the grid doubles
 // (a block's partial bytes halve; the Wv_h panel is the same).
-template <int KS8, int MAXS, int RT = 32>
+// EXACT: the launch's split count is MAXS itself (uniform key splits), so no load carries a per-split guard.  The
+// guarded form branches around every (m, l) load and waits for each in turn (9 round trips before the first partial
+// load at 4 splits); unguarded, the compiler issues them together and interleaves the partial loads with the MFMAs.
+// A load batch also holds 20 / ns k-steps instead of 20 / (the next power of two): 5 splits in 3 batches, not 5.
+template <int KS8, int MAXS, int RT = 32, bool EXACT = false>
 __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
   constexpr int KB = (20 / MAXS) < KS8 ? (20 / MAXS) : KS8;   // k-steps per load batch (<= 20 partial loads)
   __shared__ float sR[8][2][16][64];
@@ -1005,8 +1009,8 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
   const long long sstride = a.slab_rows * a.H;          // (row, head) pairs per split slab
   float w[MAXS];
   float Mx = -INFINITY, L = 0.f;
-  int ns = a.splits;
-  if (a.sk_W) {                          // the chunks this row's window spans (xattn_dma_kernel)
+  int ns = EXACT ? MAXS : a.splits;
+  if (!EXACT && a.sk_W) {                // the chunks this row's window spans (xattn_dma_kernel)
     const long long f = (long long)(a.sk_lane0 + rc / a.G) * a.n_tiles;
     ns = xsk_chunk(f + a.n_tiles - 1, a.sk_W, a.sk_P) - xsk_chunk(f, a.sk_W, a.sk_P) + 1;
   }
@@ -1460,8 +1464,29 @@ void launch_xcomb_vo(const bf16* part_u, const float* part_ml, const XPlan& plan
 #define XC_RT(KS8_, MS_)                                                                                          \
   if (rt == 16) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 16>), grid, dim3(512), 0, st, a);                  \
   else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 32>), grid, dim3(512), 0, st, a);
+#define XC_RTX(KS8_, MS_)                                                                                         \
+  if (rt == 16) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 16, true>), grid, dim3(512), 0, st, a);            \
+  else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 32, true>), grid, dim3(512), 0, st, a);
+  // uniform key splits (at most 8): the exact-count instantiations (VLOG_AMD_XCOMB_EXACT=0: the bounded ones, A/B)
+  static const int exact_env = [] {
+    const char* e = std::getenv("VLOG_AMD_XCOMB_EXACT");
+    return e ? std::atoi(e) : 1;
+  }();
+  const bool exact = exact_env && !plan.sk_W && splits >= 1 && splits <= 8;
+#define XC_EXACT(KS8_)                                                                                   \
+  switch (splits) {                                                                                      \
+    case 1: XC_RTX(KS8_, 1) break;                                                                       \
+    case 2: XC_RTX(KS8_, 2) break;                                                                       \
+    case 3: XC_RTX(KS8_, 3) break;                                                                       \
+    case 4: XC_RTX(KS8_, 4) break;                                                                       \
+    case 5: XC_RTX(KS8_, 5) break;                                                                       \
+    case 6: XC_RTX(KS8_, 6) break;                                                                       \
+    case 7: XC_RTX(KS8_, 7) break;                                                                       \
+    default: XC_RTX(KS8_, 8) break;                                                                      \
+  }
 #define XC_LAUNCH(KS8_)                                                                                  \
-  if (splits <= 1) { XC_RT(KS8_, 1) }                                                                    \
+  if (exact) { XC_EXACT(KS8_) }                                                                          \
+  else if (splits <= 1) { XC_RT(KS8_, 1) }                                                               \
   else if (splits <= 2) { XC_RT(KS8_, 2) }                                                               \
   else if (splits <= 4) { XC_RT(KS8_, 4) }                                                               \
   else if (splits <= 8) { XC_RT(KS8_, 8) }                                                               \
@@ -1475,6 +1500,8 @@ void launch_xcomb_vo(const bf16* part_u, const float* part_ml, const XPlan& plan
     default: throw std::runtime_error("xcomb_vo: unsupported n_state " + std::to_string(d));
   }
 #undef XC_LAUNCH
+#undef XC_EXACT
+#undef XC_RTX
 #undef XC_RT
   WM_LAUNCH_CHECK("xcomb_vo_kernel");
 }
