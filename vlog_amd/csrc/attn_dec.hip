@@ -813,27 +813,39 @@ __global__ __launch_bounds__(256, 2) void cross_tf_kernel(DecAttnArgs a, int gro
     g = rest / H;
   }
   const int row0 = g * group;
-  const int hyp0 = a.row_hyp[row0];
+  const int rr = qt * 128 + tid;                 // this thread's row of the liveness vote
+  const int r = qt * 128 + wv * 32 + ql;         // this lane's row of the tile
+  // The index loads in two dependent batches (row -> hypothesis -> slot / done flag), every load of a batch issued
+  // before any of them is used (loaded one at a time, between branches and the vote, they were six round trips)
+  int z = 0;                                     // opaque zero: the uniform index loads go out as vector loads
+  asm volatile("" : "+v"(z));                    // with their batch (as scalar loads they were sunk to their uses)
+  const int hyp0v = a.row_hyp[row0 + z];
+  const int hyp_t = a.row_hyp[row0 + min(rr, group - 1)];
+  const int hyp_r = a.row_hyp[row0 + min(r, group - 1)];
+  const int hmv = a.probs ? a.head_map[h + z] : -1;
+  // panels by window slot; without a slot table (the factored form's per-layer projection of the pass's windows)
+  // by the pass's window index
+  const int slotv = a.hyp_slot ? a.hyp_slot[hyp0v] : hyp0v;
+  int done_t = 0, done_r = 0;
+  if (a.done) {                                  // one branch: both flags requested together
+    done_t = a.done[hyp_t];
+    done_r = a.done[hyp_r];
+  }
+  const int slot = __builtin_amdgcn_readfirstlane(slotv), hm = __builtin_amdgcn_readfirstlane(hmv);
   // Liveness per ROW: the hypotheses of a sampling group (best_of > 1) end at different steps, so the block runs
   // while any row of its tile is live and writes only live rows (the VALU group kernel's rule)
   if (a.done) {
-    const int rr = qt * 128 + tid;
-    const bool live = tid < 128 && rr < group && !a.done[a.row_hyp[row0 + rr]];
+    const bool live = tid < 128 && rr < group && !done_t;
     if (!__syncthreads_or(live)) return;
   }
-  // panels by window slot; without a slot table (the factored form's per-layer projection of the pass's windows)
-  // by the pass's window index
-  const int slot = a.hyp_slot ? a.hyp_slot[hyp0] : hyp0;
   const long long off = ((long long)slot * H + h) * ((long long)T * HD);
   const bf16* K = a.kbase + off;
   const bf16* V = a.vbase + off;
-  const int hm = a.probs ? a.head_map[h] : -1;
   const bool cap = hm >= 0;
   if (a.stat && tid == 0)
     atomicAdd(a.stat + (blockIdx.x & (STAT_SLOTS - 1)), (unsigned long long)((cap ? 3 : 2) * T * HD * 2));
-  const int r = qt * 128 + wv * 32 + ql;
   const bool valid = r < group;
-  const bool live = valid && !(a.done && a.done[a.row_hyp[row0 + r]]);   // output writes only for live rows
+  const bool live = valid && !done_r;            // output writes only for live rows
   const bool wave_on = qt * 128 + wv * 32 < group;     // wave-uniform: a wave with no row only stages tiles
   const float sl2 = a.scale_log2;
   const int ntt = (T + TF_KT - 1) / TF_KT;

@@ -156,6 +156,8 @@ __global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
     bf16x8 qv;
     const int col = h * 64 + c8;
     if (a.q_part) {
+      // the bias first: requested with the slabs, not one more round trip after their sum
+      const f32x4 bq0 = *(const f32x4*)(a.q_bias + col), bq1 = *(const f32x4*)(a.q_bias + col + 4);
       const long long slab = (long long)a.q_rows * a.ldq;
       const float* pq = a.q_part + (long long)r * a.ldq + col;
       f32x4 lo[XMAXS], hi[XMAXS];
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(256) void xq_kernel(XQArgs a) {
           for (int i = 0; i < 4; ++i) { v[i] += lo[sp][i]; v[4 + i] += hi[sp][i]; }
         }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qv[i] = f2bf(v[i] + a.q_bias[col + i]);
+      for (int i = 0; i < 8; ++i) qv[i] = f2bf(v[i] + (i < 4 ? bq0[i] : bq1[i - 4]));
     } else {
       qv = *(const bf16x8*)(a.q + (long long)r * a.ldq + col);
     }
