@@ -531,6 +531,9 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
   load8(a.q + (long long)row * a.ldq + h * HD + sub * 8, qf);
   const int kbeg = KSPLIT ? wv * nk / 4 : 0, kend = KSPLIT ? (wv + 1) * nk / 4 : nk;
   const int* lrow = a.lin ? a.lin + (long long)hyp * a.n_ctx : nullptr;
+  // the done flag is requested here, with the first keys (read at the store: loaded there, it was one more round trip)
+  // (branch-free: without a done table the load reads the row's own hypothesis entry and is ignored)
+  const int done_v = *(a.done ? a.done + hyp : a.row_hyp + row);
   const long long hstride = (long long)H * a.n_ctx * HD;
   const bf16* K = a.kbase + (long long)h * a.n_ctx * HD + sub * 8;
   const bf16* V = a.vbase + (long long)h * a.n_ctx * HD + sub * 8;
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(256) void self_attn_wave_kernel(DecAttnArgs a, int 
     }
     m = M;
   }
-  const bool dead = a.done && a.done[hyp];
+  const bool dead = a.done && done_v != 0;
   if (a.stat && !dead && lane == 0 && (!KSPLIT || wv == 0))
     atomicAdd(a.stat + (pair & (STAT_SLOTS - 1)), (unsigned long long)(nk * 2 * HD * 2 + 2 * HD * 2));
   if constexpr (KSPLIT) {
