@@ -197,20 +197,28 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
                                      int splits) {
   const int pair = blockIdx.x;
   const int row = pair / H, h = pair - row * H;
-  if (done && done[row_hyp[row]]) return;
   const int e = threadIdx.x;
   const long long pb = (long long)pair * splits;
-  // every partial requested before any is used (a runtime loop over the splits paid one dependent round trip
-  // per split and operand: ~6 us per launch at 12 splits); sums in split order as before
+  // every load requested before any is used (a runtime loop over the splits paid one dependent round trip per split
+  // and operand: ~6 us per launch at 12 splits); sums in split order as before.  The done flag (row -> hypothesis ->
+  // flag) goes out around the partials instead of two round trips ahead of them (a finished row's partials are read
+  // and dropped).  All as vector loads from an opaque zero offset, so the compiler can neither turn the uniform
+  // ones into scalar loads waited one batch later nor hoist the flag's branch above the partials.
+  int z = 0;
+  asm volatile("" : "+v"(z));
+  // (branch-free: without a done table both loads read part_m's first word and are ignored)
+  const int hyp = *((done ? row_hyp + row : (const int*)part_m) + z);
   constexpr int SMAX = 16;
   float pm[SMAX], pl[SMAX], po[SMAX];
 #pragma unroll
   for (int s = 0; s < SMAX; ++s) {
-    const long long q = pb + (s < splits ? s : 0);
+    const long long q = pb + (s < splits ? s : 0) + z;
     pm[s] = part_m[q];
     pl[s] = part_l[q];
     po[s] = part_o[q * HD + e];
   }
+  const int flag = *(done ? done + hyp : (const int*)part_m);
+  const bool dead = done && flag;
   float M = -INFINITY;
 #pragma unroll
   for (int s = 0; s < SMAX; ++s)
@@ -223,7 +231,7 @@ __global__ void cross_combine_kernel(const float* __restrict__ part_m, const flo
       L += pl[s] * w;
       o += po[s] * w;
     }
-  out[(long long)row * ldo + h * HD + e] = f2bf(o / L);
+  if (!dead) out[(long long)row * ldo + h * HD + e] = f2bf(o / L);
 }
 
 // The key-split merge of one (row, head, element) from partials another block wrote through to L2 (agent-scope

@@ -338,6 +338,36 @@ __global__ __launch_bounds__(NW * 64) void dec_ring_kernel(GemmA a, const bf16* 
     __syncthreads();
   }
   const bool to_slab = splitk > 1 || KIND == EPI_RESID_LN;
+  // the epilogue's operands (bias chunks; DEC_QKV: each row's hypothesis and position) requested before the first
+  // store, at clamped in-bounds addresses (loaded in the fragment loop, each took its own round trip)
+  constexpr bool PRE = KIND == EPI_BF16 || KIND == EPI_DEC_QKV;
+  f32x4 bpre[NC];
+  int hpre[HALF], ppre[HALF];
+  if constexpr (PRE) {
+    if (!to_slab) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int col0 = n0 + (wc * NC + c) * 16 + 4 * (lane >> 4);
+        bpre[c] = epi.bias ? *(const f32x4*)(epi.bias + (col0 < N ? col0 : 0)) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if constexpr (KIND == EPI_DEC_QKV) {
+#pragma unroll
+        for (int i = 0; i < HALF; ++i) {
+          const int row = min(m0 + (wr * HALF + i) * 16 + (lane & 15), M - 1);
+          hpre[i] = epi.row_hyp[row];
+          ppre[i] = epi.row_pos[row];
+        }
+      }
+      // one wait for all of them here, before any store: each value re-emerges from an empty asm, so no later use
+      // carries a wait (the compiler put a vmcnt(0) at every fragment, i.e. waited for the previous one's stores)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(bpre[c]));
+      if constexpr (KIND == EPI_DEC_QKV) {
+#pragma unroll
+        for (int i = 0; i < HALF; ++i) asm volatile("" : "+v"(hpre[i]), "+v"(ppre[i]));
+      }
+    }
+  }
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int col0 = n0 + (wc * NC + c) * 16 + 4 * (lane >> 4);
@@ -379,9 +409,13 @@ __global__ __launch_bounds__(NW * 64) void dec_ring_kernel(GemmA a, const bf16* 
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[c][i][e], rs, pfc[c][e] - rm * pfs[c][e]);
-        apply_epi4<KIND>(epi, row, col0, v);
+        if constexpr (PRE) apply_epi4_pre<KIND>(epi, row, col0, v, bpre[c], hpre[KIND == EPI_DEC_QKV ? i : 0],
+                                                ppre[KIND == EPI_DEC_QKV ? i : 0]);
+        else apply_epi4<KIND>(epi, row, col0, v);
       } else {
-        apply_epi4<KIND>(epi, row, col0, acc[c][i]);
+        if constexpr (PRE) apply_epi4_pre<KIND>(epi, row, col0, acc[c][i], bpre[c], hpre[KIND == EPI_DEC_QKV ? i : 0],
+                                                ppre[KIND == EPI_DEC_QKV ? i : 0]);
+        else apply_epi4<KIND>(epi, row, col0, acc[c][i]);
       }
     }
   }
@@ -836,6 +870,25 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
         }
       }
   }
+  // the epilogue's operands (bias chunk; DEC_QKV: each row's hypothesis and position), requested behind the operand
+  // loads instead of after the reduction (there they cost one or two more round trips per launch)
+  constexpr bool PRE = KIND == EPI_BF16 || KIND == EPI_DEC_QKV;
+  f32x4 bpre = f32x4{0.f, 0.f, 0.f, 0.f};
+  int hpre[MF], ppre[MF];
+  if constexpr (PRE) {
+    if (splitk == 1 && wv == 0) {
+      const int c0 = n0 + 4 * (lane >> 4);
+      if (epi.bias) bpre = *(const f32x4*)(epi.bias + (c0 < N ? c0 : 0));
+      if constexpr (KIND == EPI_DEC_QKV) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int row = min(i * 16 + (lane & 15), M - 1);
+          hpre[i] = epi.row_hyp[row];
+          ppre[i] = epi.row_pos[row];
+        }
+      }
+    }
+  }
   f32x4 acc[MF];
 #pragma unroll
   for (int i = 0; i < MF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -887,6 +940,15 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
     }
     return;
   }
+  if constexpr (PRE) {                   // one wait for the prefetched operands, none at the fragments' stores
+    if (!to_slab) {
+      asm volatile("" : "+v"(bpre));
+      if constexpr (KIND == EPI_DEC_QKV) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) asm volatile("" : "+v"(hpre[i]), "+v"(ppre[i]));
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
     f32x4 v = sred[0][i][lane];
@@ -896,6 +958,8 @@ __global__ __launch_bounds__(NWV * 64) void gemv_dec_kernel(GemmA a, const bf16*
     if (row >= M || col0 >= N) continue;
     if (to_slab)
       *(f32x4*)(part + ((long long)split * M + row) * N + col0) = v;
+    else if constexpr (PRE)
+      apply_epi4_pre<KIND>(epi, row, col0, v, bpre, hpre[KIND == EPI_DEC_QKV ? i : 0], ppre[KIND == EPI_DEC_QKV ? i : 0]);
     else
       apply_epi4<KIND>(epi, row, col0, v);
   }

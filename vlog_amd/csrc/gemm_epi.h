@@ -133,6 +133,48 @@ __device__ __forceinline__ void apply_epi4(const GemmEpi& epi, int row, int col0
   }
 }
 
+// apply_epi4 with its loaded operands passed in: the bias chunk `b` (used only when epi.bias is set) and, for
+// EPI_DEC_QKV, the row's hypothesis and position.  A kernel that stores several fragments requests these for all of
+// them before the first store (inside the fragment loop each load waited for its own round trip); the arithmetic is
+// apply_epi4's.
+template <int KIND>
+__device__ __forceinline__ void apply_epi4_pre(const GemmEpi& epi, int row, int col0, f32x4 acc, f32x4 b, int hyp,
+                                               int pos) {
+  if constexpr (KIND == EPI_BF16 || KIND == EPI_DEC_QKV) {
+    f32x4 v = acc;
+    if (epi.bias) v += b;
+    if constexpr (KIND == EPI_BF16) {
+      if (epi.act == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      }
+      long long o = epi.rpb ? (long long)(row / epi.rpb) * epi.bstride + (long long)(row % epi.rpb + epi.roff) * epi.ldc
+                            : (long long)row * epi.ldc;
+      bf16x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = f2bf(v[e]);
+      *(bf16x4*)((bf16*)epi.out + o + col0) = r;
+    } else {
+      const int d = epi.d;
+      bf16x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = f2bf(v[e]);
+      if (col0 < d) {
+        *(bf16x4*)((bf16*)epi.out + (long long)row * epi.ldc + col0) = r;
+      } else {
+        const int c2 = col0 - d;
+        const int kv = c2 >= d;
+        const int cc = kv ? c2 - d : c2;
+        const int h = cc / epi.head_dim, e2 = cc - h * epi.head_dim;
+        const long long slot = (((long long)hyp * epi.n_head + h) * epi.n_ctx + pos) * epi.head_dim + e2;
+        *(bf16x4*)((kv ? epi.vcache : epi.kcache) + slot) = r;
+      }
+    }
+  } else {
+    apply_epi4<KIND>(epi, row, col0, acc);
+  }
+}
+
 // ---- Staged epilogue helpers (gemm_8p.hip): the value of 4 consecutive outputs (bias / activation /
 // positional add folded in, same arithmetic as apply_epi4), and whole 16-B chunk stores of it.
 template <int KIND>
