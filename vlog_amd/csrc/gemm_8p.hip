@@ -236,6 +236,16 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
   constexpr bool BF16_OUT = KIND == EPI_BF16 || KIND == EPI_CROSS_KV;
   constexpr bool F32_OUT = KIND == EPI_RESID_F32 || KIND == EPI_F32 || KIND == EPI_GELU_POS_F32;
   if (BF16_OUT && N % 8 == 0 && epi.ldc % 8 == 0 && (epi.rpb == 0 || epi.bstride % 8 == 0 || KIND == EPI_CROSS_KV)) {
+    // this lane's 4 bias chunks (one per column fragment j), requested together and waited once: epi_value4 loaded
+    // the chunk for each of the 32 fragments and waited for it (32 dependent L2 round trips per tile epilogue)
+    f32x4 bj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col0 = min(n0 + wn * 64 + j * 16 + 4 * fq, N - 4);
+      bj[j] = epi.bias ? *(const f32x4*)(epi.bias + col0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(bj[j]));
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int rl = wm * 128 + i * 16 + fr;
@@ -243,7 +253,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
       for (int j = 0; j < 4; ++j) {
         const int cl = wn * 64 + j * 16 + 4 * fq;
         const int col0 = min(n0 + cl, N - 4);
-        const f32x4 v = epi_value4<KIND>(epi, m0 + rl, col0, acc[i][j]);
+        const f32x4 v = epi_value4_pre<KIND>(epi, m0 + rl, col0, acc[i][j], bj[j]);
         bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
@@ -276,14 +286,18 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
         }
       }
       if (wm == half) {
+        // column fragment outermost: its bias chunk is loaded once for the 8 row fragments (registers are short here:
+        // the residual chunks above are live), 4 round trips per half instead of 32
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int rl = i * 16 + fr;
+        for (int j = 0; j < 4; ++j) {
+          const int cl = wn * 64 + j * 16 + 4 * fq;
+          const int col0 = min(n0 + cl, N - 4);
+          const f32x4 b = (KIND != EPI_GELU_POS_F32 && epi.bias) ? *(const f32x4*)(epi.bias + col0)
+                                                                 : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int cl = wn * 64 + j * 16 + 4 * fq;
-            const int col0 = min(n0 + cl, N - 4);
-            *(f32x4*)(sf + rl * P8_SR32 + cl) = epi_value4<KIND>(epi, m0 + half * 128 + rl, col0, acc[i][j]);
+          for (int i = 0; i < 8; ++i) {
+            const int rl = i * 16 + fr;
+            *(f32x4*)(sf + rl * P8_SR32 + cl) = epi_value4_pre<KIND>(epi, m0 + half * 128 + rl, col0, acc[i][j], b);
           }
         }
       }

@@ -197,6 +197,24 @@ __device__ __forceinline__ f32x4 epi_value4(const GemmEpi& epi, int row, int col
   return v;
 }
 
+// epi_value4 with the bias chunk `b` loaded ahead (used only when epi.bias is set): a kernel whose fragments share
+// a few columns requests those chunks once, before its fragment loop (loaded per fragment, each load waited for its
+// own round trip).  GELU_POS still loads its positional row per fragment.
+template <int KIND>
+__device__ __forceinline__ f32x4 epi_value4_pre(const GemmEpi& epi, int row, int col0, f32x4 acc, f32x4 b) {
+  if constexpr (KIND == EPI_GELU_POS_F32) {
+    return epi_value4<KIND>(epi, row, col0, acc);
+  } else {
+    f32x4 v = acc;
+    if (epi.bias) v += b;
+    if (KIND == EPI_BF16 && epi.act == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+    }
+    return v;
+  }
+}
+
 // 8 consecutive bf16 outputs (col0 % 8 == 0) of a bf16-output kind
 template <int KIND>
 __device__ __forceinline__ void epi_store8_bf16(const GemmEpi& epi, int row, int col0, bf16x8 v) {
