@@ -271,6 +271,12 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
   }
   if (F32_OUT && epi.ldc % 4 == 0) {
     float* sf = (float*)smem;
+    // RESID_F32 / F32: the bias is added in the store loop, where a thread's column is the same for every k and
+    // both halves (c & 63 = tid & 63): one chunk, requested here, instead of loads between the staging writes
+    // (half 1's waited for half 0's store acknowledgements: vmcnt counts stores).  v = acc + b as epi_value4.
+    constexpr bool BIAS_AT_STORE = KIND == EPI_RESID_F32 || KIND == EPI_F32;
+    f32x4 bS = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS_AT_STORE && epi.bias) bS = *(const f32x4*)(epi.bias + min(n0 + (tid & 63) * 4, N - 4));
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       // RESID_F32: this thread's 16 residual chunks of the half are loaded before the staging (one memory round
@@ -286,18 +292,15 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
         }
       }
       if (wm == half) {
-        // column fragment outermost: its bias chunk is loaded once for the 8 row fragments (registers are short here:
-        // the residual chunks above are live), 4 round trips per half instead of 32
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int cl = wn * 64 + j * 16 + 4 * fq;
           const int col0 = min(n0 + cl, N - 4);
-          const f32x4 b = (KIND != EPI_GELU_POS_F32 && epi.bias) ? *(const f32x4*)(epi.bias + col0)
-                                                                 : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int rl = i * 16 + fr;
-            *(f32x4*)(sf + rl * P8_SR32 + cl) = epi_value4_pre<KIND>(epi, m0 + half * 128 + rl, col0, acc[i][j], b);
+            *(f32x4*)(sf + rl * P8_SR32 + cl) =
+                BIAS_AT_STORE ? acc[i][j] : epi_value4<KIND>(epi, m0 + half * 128 + rl, col0, acc[i][j]);
           }
         }
       }
@@ -307,7 +310,8 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmA a, const bf16* __
         const int c = tid + 512 * k, rl = c >> 6, cc = (c & 63) * 4;
         const int row = m0 + half * 128 + rl, col0 = n0 + cc;
         if (row < M && col0 < N) {
-          const f32x4 v = *(const f32x4*)(sf + rl * P8_SR32 + cc);
+          f32x4 v = *(const f32x4*)(sf + rl * P8_SR32 + cc);
+          if (BIAS_AT_STORE && epi.bias) v += bS;
           if (KIND == EPI_RESID_F32) *(f32x4*)((float*)epi.out + (long long)row * epi.ldc + col0) = res[k] + v;
           else epi_store4_f32<KIND>(epi, row, col0, v);
         }
