@@ -994,7 +994,7 @@ struct XCombArgs {
 // RT = rows per block, 32 or 16.  With 16, MFMA rows 16..31 repeat rows 0..15 (same addresses: no extra bytes)
 // and are not stored, so every output keeps the 32-row form's arithmetic bit for bit while the grid doubles
 // (a block's partial bytes halve; the Wv_h panel is the same).
-// EXACT: the launch's split count is MAXS itself (uniform key splits), so no load carries a per-split guard.  The
+// EXACT (opt-in, see launch_xcomb_vo): the launch's split count is MAXS itself, so no load carries a per-split guard.  The
 // guarded form branches around every (m, l) load and waits for each in turn (9 round trips before the first partial
 // load at 4 splits); unguarded, the compiler issues them together and interleaves the partial loads with the MFMAs.
 // A load batch also holds 20 / ns k-steps instead of 20 / (the next power of two): 5 splits in 3 batches, not 5.
@@ -1469,10 +1469,13 @@ void launch_xcomb_vo(const bf16* part_u, const float* part_ml, const XPlan& plan
 #define XC_RTX(KS8_, MS_)                                                                                         \
   if (rt == 16) hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 16, true>), grid, dim3(512), 0, st, a);            \
   else hipLaunchKernelGGL((xcomb_vo_kernel<KS8_, MS_, 32, true>), grid, dim3(512), 0, st, a);
-  // uniform key splits (at most 8): the exact-count instantiations (VLOG_AMD_XCOMB_EXACT=0: the bounded ones, A/B)
+  // uniform key splits (at most 8): the exact-count instantiations, opt-in (VLOG_AMD_XCOMB_EXACT=1).  5-13 % faster
+  // merges (profiles/ab_r06_xcomb_exact.jsonl), same tokens on the bench workloads, but NOT the same bits: without
+  // the per-split guards the compiler fuses the weight products differently, so the alignment heads' probabilities
+  // move in the last bits, and tests/test_gpu_words.py's batched-vs-single-window near-ties flipped (7 of 8 words).
   static const int exact_env = [] {
     const char* e = std::getenv("VLOG_AMD_XCOMB_EXACT");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   const bool exact = exact_env && !plan.sk_W && splits >= 1 && splits <= 8;
 #define XC_EXACT(KS8_)                                                                                   \
