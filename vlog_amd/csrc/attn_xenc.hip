@@ -1022,13 +1022,22 @@ __global__ __launch_bounds__(512) void xcomb_vo_kernel(XCombArgs a) {
     // every load is issued regardless of the row's state (rows past the end clamped; a finished row's
     // partials are stale but finite, and its output is never stored), so nothing waits on `done`
     const float* ml = a.part_ml + 2 * ((long long)rc * a.H + h);
+    // every (m, l) pair requested before any is used, at a clamped split index (loaded behind the per-split guards,
+    // each waited for the one before it: up to 9 round trips); the arithmetic below keeps its guards and order
+    float pm[MAXS], pl[MAXS];
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      const int sc = min(s, ns - 1);
+      pm[s] = ml[2 * sc * sstride];
+      pl[s] = ml[2 * sc * sstride + 1];
+    }
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
-      if (s < ns) Mx = fmaxf(Mx, ml[2 * s * sstride]);
+      if (s < ns) Mx = fmaxf(Mx, pm[s]);
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
       if (s < ns) {
-        w[s] = ml[2 * s * sstride + 1] * __builtin_amdgcn_exp2f(ml[2 * s * sstride] - Mx);
+        w[s] = pl[s] * __builtin_amdgcn_exp2f(pm[s] - Mx);
         L += w[s];
       }
     const float inv = 1.0f / L;
